@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the MI355X volume ray-marcher on BASELINE.json's metric configuration.
+
+Workload (BASELINE.json `metric`, SURVEY.md 8d "north-star metric config"): V_shell(1024) fp32
+volume (synthetic, generated in HBM), 1920x1080 image, Henyey-Greenstein shading with the two
+lights of examples/example1.m:36, on-the-fly gradient, Fe=1 Fr=0.4 Fa=0.6, color [1 1 0],
+threshold 0.9, camera rotate(125,25,0), f=3, dist=6, reflection = the class default Volume(1).
+
+A "step" = one frame: the ray-march kernel over this rank's image columns (+ at N>1 the RCCL
+gather of the column partitions to rank 0 and the on-device assembly of the full image).
+Volumes are resident in HBM before the timed region (sync_volumes is not timed).
+Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Mrays/s + achieved HBM GB/s, 1024³ vol @ 1920×1080 HG-shaded, 1/2/4/8 GPU"
+
+
+def rotation(alpha, beta, gamma):
+    """VolumeRender.rotate from identity (exact cosd/sind at multiples of 90)."""
+    from volume_renderer_amd.volume_render import _cosd, _sind
+    ca, sa, cb, sb, cg, sg = _cosd(alpha), _sind(alpha), _cosd(beta), _sind(beta), _cosd(gamma), _sind(gamma)
+    rx = np.array([[1, 0, 0], [0, ca, -sa], [0, sa, ca]])
+    ry = np.array([[cb, 0, sb], [0, 1, 0], [-sb, 0, cb]])
+    rz = np.array([[cg, -sg, 0], [sg, cg, 0], [0, 0, 1]])
+    return np.eye(3) @ rx @ ry @ rz
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1024, help="volume edge (metric config: 1024)")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--block-cols", type=int, default=16, help="column block of the image partition")
+    ap.add_argument("--cpu-stride", type=int, default=16, help="CPU baseline: every k-th column")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run --nproc-per-node N")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import volume_renderer_amd as vr
+    from volume_renderer_amd import mex
+
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    n, W, H = args.n, args.width, args.height
+
+    # ---- inputs, resident in HBM before timing ------------------------------------------------
+    vol_t = torch.empty(n * n * n, dtype=torch.float32, device=dev)
+    mex.synth_shell_device(vol_t.data_ptr(), n, sptr)
+    torch.cuda.synchronize(dev)
+    em = mex.DeviceVolume(vol_t.data_ptr(), (n, n, n), last_update=10, owner=vol_t)
+    refl = vr.Volume(1)          # VolumeRender.m:131 default VolumeReflection
+    refl.TimeLastUpdate = np.uint64(5)
+    lut = vr.Volume(vr.HenyeyGreenstein(64))
+    lut.TimeLastUpdate = np.uint64(7)
+    lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+    h = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)  # Em, Re, Ab (Ab aliases Em)
+    R = rotation(125, 25, 0)
+    ra, keep = mex.render_args(lights, lut, np.float32([1.0, 0.4, 0.6]), np.float32([1, 1, 1]),
+                               np.uint64([H, W]), np.flip(R, 0).astype(np.float32), np.float32([0, 3.0, 6.0]),
+                               np.float32(0.9), np.float32([1, 1, 0]))
+    host_vol = vol_t.cpu().numpy() if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
+    del vol_t  # the library holds its own resident copy
+
+    part = mex.partition(args.block_cols, rank, world) if world > 1 else None
+    my_cols = mex.partition_columns(W, part)
+    max_cols = max(mex.partition_columns(W, mex.partition(args.block_cols, p, world)) for p in range(world)) \
+        if world > 1 else W
+    out_local = torch.zeros(3 * max_cols * H, dtype=torch.float32, device=dev)
+    full = torch.zeros(3 * W * H, dtype=torch.float32, device=dev) if rank == 0 else None
+    gathered = (torch.zeros(world * 3 * max_cols * H, dtype=torch.float32, device=dev)
+                if (world > 1 and rank == 0) else None)
+    steps_t = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    # sample count of this rank's launch (exact, counter variant; untimed)
+    mex.render_device(h, ra, out_local.data_ptr(), part, steps_t.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    my_samples = int(steps_t.item())
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def frame(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        mex.render_device(h, ra, out_local.data_ptr(), part, 0, sptr)
+        if i is not None:
+            ev[i][1].record(stream)
+        if world > 1:
+            dist.gather(out_local, list(gathered.chunk(world)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                mex.assemble_partitions(gathered.data_ptr(), W, H, args.block_cols, world, max_cols,
+                                        full.data_ptr(), sptr)
+
+    for _ in range(args.warmup):
+        frame()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        frame(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    samples_all = torch.tensor([my_samples], dtype=torch.int64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(samples_all, op=dist.ReduceOp.SUM)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_samples = int(samples_all.item())
+
+    result = None
+    if rank == 0:
+        rays = W * H
+        ms_per_step = elapsed / args.steps * 1e3
+        value = rays * args.steps / elapsed / 1e6
+        L, G = 2, 6
+        F = 1 + (G + 1 + L)  # trilinear fetches per sample, SURVEY.md 8d
+        bytes_launch = 4.0 * my_samples * F + 12.0 * my_cols * H
+        achieved = bytes_launch / t_kernel_s / 1e9
+        result = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic V_shell(%d) (SURVEY.md 8d), generated in HBM" % n,
+            "config": {"workload": f"V_shell({n}) fp32 {n}^3, {W}x{H}, HG 2 lights (example1.m), on-the-fly "
+                                   "gradient, rotate(125,25,0) f=3 dist=6 thr=0.9",
+                       "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": "compute",
+                       "parallelism": f"image-column partition x{world} (block {args.block_cols})"
+                       + (" + RCCL gather" if world > 1 else "")},
+            "samples_per_frame": total_samples,
+            "gb_per_s_sample_stream": round(4.0 * total_samples * F / (elapsed / args.steps) / 1e9, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(t_kernel_s * 1e3, 3),
+                         "bytes_per_launch": bytes_launch,
+                         "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F},
+            "cpu_baseline": None,
+        }
+
+    # ---- CPU baseline: the oracle (C, OpenMP) on every k-th column of the same frame -----------
+    if rank == 0 and world == 1 and host_vol is not None:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        S = O.OracleSession()
+        oh = S.new()
+        ovol = O.OVolume(host_vol.reshape((n, n, n), order="F"), 10)
+        S.sync_volumes(oh, 0, ovol, O.OVolume(refl.Data, 5), ovol)
+        L6 = np.array([list(l.Position) + list(l.Color) for l in lights], np.float32)
+        cols = np.arange(0, W, args.cpu_stride, dtype=np.int64)
+        t1 = time.perf_counter()
+        img, cpu_samples = S.render(oh, L6, O.OVolume(lut.Data, 7), [1.0, 0.4, 0.6], [1, 1, 1], [H, W],
+                                    np.flip(R, 0).astype(np.float32), [0, 3.0, 6.0], 0.9, [1, 1, 0],
+                                    threads=threads, cols=cols)
+        cpu_s = time.perf_counter() - t1
+        gpu_img = full if full is not None and world > 1 else out_local
+        g = gpu_img[: 3 * W * H].view(3, W, H).cpu().numpy()
+        o = np.transpose(img, (2, 1, 0))  # [H,W,3] F-order -> (3, W, H) C-order view
+        d = np.abs(g[:, cols, :] - o[:, cols, :])
+        result["cpu_baseline"] = {
+            "value": round(len(cols) * H / cpu_s / 1e6, 5), "unit": "Mrays/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/vr_oracle.c (scalar C restatement, OpenMP) on every {args.cpu_stride}th column "
+                      f"({len(cols)} cols x {H} rays, {cpu_samples} samples) of the same frame, {cpu_s:.1f} s"}
+        result["parity_sampled_columns"] = {
+            "max_abs": float(d.max()), "img_max": float(np.abs(o[:, cols, :]).max()),
+            "bit_exact_frac": float((g[:, cols, :].view(np.uint32) == o[:, cols, :].view(np.uint32)).mean())}
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    vr.volumeRender("delete", h)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * vrhip.h -- C-ABI of libvrhip.so, the MI355X (gfx950) volume ray-marcher.
+ *
+ * The entry points mirror, one for one, the command protocol of the reference's CUDA mex
+ * `volumeRender` (/root/reference/src/C/mex/render.cpp:50-278) plus its two helper mex files, so
+ * that a thin mexFunction adaptor (mex/volumeRender_mex.cpp) keeps the MATLAB
+ * classes VolumeRender / Volume / LightSource working unchanged.  Plain pointers and sizes only.
+ *
+ * Conventions (identical to what the mex receives from MATLAB):
+ *   - volumes are MATLAB single arrays Data(d0,d1,d2), column-major, d0 fastest; a 2-D array has
+ *     d2 = 1 (volumeRender.cpp:320-339).  Data pointers are borrowed for the call only.
+ *   - the rendered image is MATLAB single [H, W, 3], column-major: out[x*H + y + c*W*H]
+ *     (volumeRender_kernel.cu:496-506, render.cpp:248).
+ *   - every function returns VR_OK (0) or an error code; vr_last_error() gives the message
+ *     (the reference's mexErrMsgTxt text where one exists).  Errors are thread-local.
+ */
+#ifndef VRHIP_H_
+#define VRHIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum vr_status {
+  VR_OK = 0,
+  VR_ERR_ARGUMENT = 1,   /* bad argument count/shape (render.cpp:51-56,60-61,68-69,136-140) */
+  VR_ERR_HANDLE = 2,     /* "Handle not valid." (class_handle.hpp:64-72)                      */
+  VR_ERR_VRAM = 3,       /* "insufficient free VRAM!" (mmanager.hxx:144-173)                   */
+  VR_ERR_DEVICE = 4,     /* a HIP runtime error (reference ignores them, common.h:43-47)        */
+  VR_ERR_UNSUPPORTED = 5 /* request outside what this build implements                          */
+};
+
+/* Where vr_volume.data lives. */
+enum vr_location { VR_HOST = 0, VR_DEVICE = 1 };
+
+/* A MATLAB `Volume` as the mex reads it (mxMake_volume, volumeRender.cpp:307-342):
+ * Data (single), its dims, and TimeLastUpdate.  `location` VR_DEVICE lets device-resident data
+ * (e.g. a torch tensor) be synced without a host round trip. */
+typedef struct vr_volume {
+  const float *data;
+  uint64_t dims[3];      /* d0, d1, d2 (d2 = 1 for 2-D data)          */
+  uint64_t last_update;  /* TimeLastUpdate (ms timestamp, see vr_timestamp) */
+  int32_t location;      /* enum vr_location                           */
+  int32_t reserved;
+} vr_volume;
+
+/* A MATLAB `LightSource` (LightSource.m:40-64): Position and Color exactly as stored in MATLAB.
+ * The position is reversed into kernel order internally (render.cpp:167-168). */
+typedef struct vr_light {
+  float position[3];
+  float color[3];
+} vr_light;
+
+/* The positional arguments of volumeRender('render', h, ...) (render.cpp:142-240,
+ * caller VolumeRender.m:563-581), in the order and units MATLAB passes them. */
+typedef struct vr_render_args {
+  const vr_light *lights;         /* LightSources (prhs[2])                                  */
+  int64_t num_lights;             /* mxGetN(LightSources); < 0: the logical `false`           */
+  const vr_volume *illumination;  /* VolumeIllumination (prhs[3]); NULL: the logical `false`  */
+  float factors[3];               /* single([FactorEmission FactorReflection FactorAbsorption]) */
+  float element_size_um[3];       /* single(ElementSizeUm), MATLAB order (reversed inside)    */
+  uint64_t resolution[2];         /* uint64([H W]) = flip(ImageResolution)                    */
+  float rotation_flipped[9];      /* single(flip(RotationMatrix)), column-major as passed      */
+  float props[3];                 /* single([CameraXOffset FocalLength DistanceToObject])     */
+  float opacity_threshold;        /* single(OpacityThreshold)                                 */
+  float color[3];                 /* single(Color)                                            */
+} vr_render_args;
+
+/* Image-space partition for multi-GPU rendering: columns are cut into blocks of
+ * `block_cols`; block b belongs to part (b % num_parts).  A part's output is the column-major
+ * planar image of only its columns, in increasing x, with a fixed column stride max_cols =
+ * vr_partition_columns(w, {block_cols, part 0, num_parts}) (part 0 owns the most columns):
+ * element (y, local column j, channel c) at c*max_cols*H + j*H + y. */
+typedef struct vr_partition {
+  int32_t block_cols;
+  int32_t part;
+  int32_t num_parts;
+  int32_t reserved;
+} vr_partition;
+
+typedef struct vr_context vr_context; /* the reference's MManager handle (mmanager.hxx:25) */
+
+/* --- the mex commands --------------------------------------------------------------------- */
+
+/* 'new' (render.cpp:58-65): a persistent handle bound to the current HIP device. */
+int vr_new(vr_context **out);
+
+/* 'delete' (render.cpp:72-79 -> ~MManager, mmanager.hxx:103-105).  Like the reference's
+ * cudaDeviceReset this frees every handle's device volumes and resets the module-global render
+ * state (texture bindings, slot indices, lights, gradient method). */
+int vr_delete(vr_context *h);
+
+/* 'mem_info' (render.cpp:85-87, mmanager.hxx:218-284): writes the report into buf. */
+int vr_mem_info(vr_context *h, char *buf, size_t buflen);
+
+/* 'sync_volumes' (render.cpp:93-129): note the order Emission, Reflection, Absorption.
+ * dx, dy, dz all non-NULL: the 9-argument form (gradient lookup); all NULL: the 6-argument form
+ * (gradient volumes reset, on-the-fly gradient). */
+int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume *emission,
+                    const vr_volume *reflection, const vr_volume *absorption, const vr_volume *dx,
+                    const vr_volume *dy, const vr_volume *dz);
+
+/* 'render' (render.cpp:134-277): renders into the caller-owned host image out[H*W*3]. */
+int vr_render(vr_context *h, const vr_render_args *args, float *out);
+
+/* --- the helper mex files ------------------------------------------------------------------- */
+
+/* HenyeyGreenstein(N[, g]) (HenyeyGreenstein.cc:29-96): out[N*N*N], MATLAB array (b, a, c). */
+int vr_henyey_greenstein(uint32_t n, float g, float *out);
+
+/* timestamp (timestamp.cpp:17-33): ms since the epoch, low 32 bits only (it is stored through an
+ * int*), zero-extended -- exactly the value the reference hands to MATLAB. */
+uint64_t vr_timestamp(void);
+
+/* --- device-side extensions (multi-GPU, benchmarking; no MATLAB counterpart) ------------------ */
+
+/* 'render' without the host round trip: writes the (partitioned, if part != NULL) image to the
+ * device buffer d_out on `stream` (a hipStream_t; NULL = default stream).  Asynchronous.
+ * If d_steps != NULL, the total number of ray-march samples is atomically added to *d_steps. */
+int vr_render_device(vr_context *h, const vr_render_args *args, const vr_partition *part,
+                     float *d_out, unsigned long long *d_steps, void *stream);
+
+/* Number of columns a part owns for image width w. */
+int64_t vr_partition_columns(int64_t w, const vr_partition *part);
+
+/* Scatter gathered part images (num_parts slabs of max_cols*H*3 floats each, part p at
+ * d_parts + p*max_cols*H*3) into the full [H, W, 3] image d_out, on `stream`. */
+int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t block_cols,
+                           int32_t num_parts, int64_t max_cols, float *d_out, void *stream);
+
+/* Synthetic test volume V_shell(n) of SURVEY.md 8d, generated on the device into d_out[n^3]. */
+int vr_synth_shell_device(float *d_out, uint64_t n, void *stream);
+
+/* Host-side reproduction of the upload/slot state machine (syncWithDevice,
+ * volumeRender_kernel.cu:739-867) for unit tests: returns the slot indices after a sync with the
+ * given similarity/update flags starting from `idx` (emission, absorption, reflection). */
+int vr_debug_slot_transition(const int32_t idx_in[3], int32_t sim_em_ab, int32_t sim_em_re,
+                             int32_t sim_ab_re, int32_t req_em, int32_t req_ab, int32_t req_re,
+                             int32_t idx_out[3], int32_t unbound_out[3]);
+
+/* Last error message of this thread ("" if none). */
+const char *vr_last_error(void);
+
+/* Library build identification ("libvrhip <version> gfx950 ..."). */
+const char *vr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VRHIP_H_ */

@@ -1,0 +1,275 @@
+"""GPU parity: the HIP path (libvrhip via the Python mirror of the MATLAB API) against the CPU
+oracle, scenario by scenario, through the harness in tests/harness.py.  Scenarios follow the
+reference's examples (examples/example1.m, example1_grad.m, example3.m) and the golden-vector
+plan of SURVEY.md 8c (EA-only, HG 1 & 2 lights, lookup gradient, stereo, absorption aliasing,
+slot stickiness, several handles, delete semantics, edge cases)."""
+import gc
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+vr = pytest.importorskip("volume_renderer_amd")
+
+
+@pytest.fixture(autouse=True)
+def _clean():
+    gc.collect()
+    yield
+    gc.collect()
+
+
+def ex1_renderer(vol_em, res=(96, 80), lights=True, thr=0.9):
+    """examples/example1.m:32-58 set-up on synthetic data."""
+    r = vr.VolumeRender()
+    if lights:
+        r.VolumeIllumination = vr.Volume(vr.HenyeyGreenstein(64))
+        r.LightSources = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+    r.ElementSizeUm = [1, 1, 1]
+    r.FocalLength = 3.0
+    r.DistanceToObject = 6
+    r.rotate(125, 25, 0)
+    r.OpacityThreshold = thr
+    r.ImageResolution = list(res)
+    r.VolumeEmission = vol_em
+    r.VolumeAbsorption = vol_em
+    r.FactorAbsorption = 0.6
+    r.FactorReflection = 0.4
+    r.Color = [1, 1, 0]
+    return r
+
+
+def test_c1_emission_absorption_only(monkeypatch, counter_clock):
+    """BASELINE config 1: V_shell(64), 256x256, emission-absorption only."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(64))
+    r = ex1_renderer(v, res=(256, 256), lights=False)
+    img = r.render()
+    assert img.shape == (256, 256, 3)
+    assert img.max() > 0
+    st = tee.renders[-1][2]
+    print("C1 parity", st)
+    r.delete()
+
+
+def test_hg_two_lights_compute_gradient(monkeypatch, counter_clock):
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(48))
+    r = ex1_renderer(v, res=(96, 80))
+    img = r.render()
+    assert np.isfinite(img).all() and img.max() > 0
+    print("HG2 parity", tee.renders[-1][2])
+    # second image of example1.m: new emission, separate (aliased-away) absorption, new factors
+    v2 = vr.Volume(O.shell_volume(48) * np.float32(0.5))
+    ab = vr.Volume(O.rand_volume(24))
+    r.VolumeEmission = v2
+    r.VolumeAbsorption = ab
+    r.FactorEmission = 0.1
+    r.FactorAbsorption = 0.4
+    r.FactorReflection = 0.1
+    r.Color = [1, 1, 1]
+    r.render()
+    r.delete()
+
+
+def test_lookup_gradient_then_compute(monkeypatch, counter_clock):
+    """examples/example1_grad.m: precomputed gradient volumes, then resetGradientVolumes."""
+    from harness import install
+    install(monkeypatch)
+    v = vr.Volume(O.shell_volume(40))
+    gx, gy, gz = v.grad()
+    r = ex1_renderer(v, res=(72, 64))
+    r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = gx, gy, gz
+    a = r.render()
+    r.resetGradientVolumes()
+    b = r.render()
+    assert not np.array_equal(a, b)
+    r.delete()
+
+
+def test_grad_matches_matlab_gradient(counter_clock):
+    d = O.rand_volume(12)
+    gx, gy, gz = vr.Volume(d).grad()
+    ox, oy, oz = O.matlab_gradient(d)
+    for g, o in ((gx, ox), (gy, oy), (gz, oz)):
+        assert np.array_equal(g.Data, o)
+
+
+@pytest.mark.parametrize("mode", ["RedCyan", "LeftRightHorizontal"])
+def test_stereo(monkeypatch, counter_clock, mode):
+    """VolumeRender.render off-axis stereo (VolumeRender.m:277-307), example3.m camera."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(40))
+    r = vr.VolumeRender()
+    r.VolumeIllumination = vr.Volume(vr.HenyeyGreenstein(32))
+    r.LightSources = vr.LightSource([-15, 15, 0], [0.5, 0.5, 0.5])
+    r.FocalLength = 4.5
+    r.DistanceToObject = 6
+    r.OpacityThreshold = 0.95
+    r.rotate(90, 0, 0)
+    r.rotate(-15, 15, 15)
+    r.VolumeAbsorption = v
+    r.VolumeEmission = v
+    r.ImageResolution = [80, 72]
+    r.CameraXOffset = 0.06 * 20  # large offset so that delta > 0 at this small size
+    r.StereoOutput = getattr(vr.StereoRenderMode, mode)
+    img = r.render()
+    assert len(tee.renders) == 2
+    delta = int(np.floor(0.6 * 72 / 2 + 0.5))
+    right, left = tee.renders[0][0], tee.renders[1][0]
+    assert right.shape == (72, 80 + delta, 3)
+    if mode == "RedCyan":
+        assert img.shape == (72, 80, 3)
+        assert np.array_equal(img[:, :, 0], left[:, delta:, 0])
+        assert np.array_equal(img[:, :, 1:], right[:, :80, 1:])
+    else:
+        assert img.shape == (72, 160, 3)
+    r.delete()
+
+
+def test_absorption_volume_is_never_sampled(monkeypatch, counter_clock):
+    """d_idxAbsorption stays `emission`; a distinct Absorption volume must not
+    change the image."""
+    from harness import install
+    install(monkeypatch)
+    v = vr.Volume(O.shell_volume(32))
+    r = ex1_renderer(v, res=(64, 48))
+    a = r.render()
+    r.VolumeAbsorption = vr.Volume(O.rand_volume(32))
+    b = r.render()
+    assert np.array_equal(a, b)
+    r.delete()
+
+
+def test_slot_stickiness(monkeypatch, counter_clock):
+    """Emission == Reflection makes d_idxReflection `emission`; it stays so after Emission changes
+    (kernel.cu:771-774 and no reset), so reflection then samples the NEW emission volume."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(32))
+    r = ex1_renderer(v, res=(64, 48))
+    r.VolumeReflection = v
+    r.VolumeAbsorption = v
+    r.VolumeEmission = v
+    r.render()
+    r.VolumeEmission = vr.Volume(O.shell_volume(32) * np.float32(0.7))
+    r.render()
+    # Emission == Absorption with only Reflection re-stamped: the simEmAb typo path
+    # (kernel.cu:853-856) routes emission through the reflection texture.
+    r.VolumeReflection = vr.Volume(O.rand_volume(16))
+    r.render()
+    assert len(tee.renders) == 3
+    r.delete()
+
+
+def test_two_handles_share_module_state(monkeypatch, counter_clock):
+    from harness import install
+    install(monkeypatch)
+    v1 = vr.Volume(O.shell_volume(32))
+    v2 = vr.Volume(O.rand_volume(20))
+    r1 = ex1_renderer(v1, res=(48, 40))
+    r2 = ex1_renderer(v2, res=(40, 48), lights=False)
+    r1.render()
+    r2.render()
+    r1.render()  # nothing changed for r1: textures are still bound to r2's volumes
+    r2.delete()  # cudaDeviceReset: everything unbound
+    img = r1.render()
+    assert not img.any()
+    r1.delete()
+
+
+@pytest.mark.parametrize("case", ["inside", "miss", "tiny", "aniso", "flat2d", "onevoxel", "nan"])
+def test_edge_cases(monkeypatch, counter_clock, case):
+    from harness import install
+    install(monkeypatch)
+    data = O.shell_volume(24)
+    res = (40, 30)
+    r = None
+    if case == "inside":      # camera inside the box: tnear < 0 -> 0
+        r = ex1_renderer(vr.Volume(data), res=res)
+        r.DistanceToObject = 0.2
+    elif case == "miss":      # most rays miss the box
+        r = ex1_renderer(vr.Volume(data), res=res)
+        r.FocalLength = 0.2
+        r.DistanceToObject = 40
+    elif case == "tiny":      # 1x1 image
+        r = ex1_renderer(vr.Volume(data), res=(1, 1))
+    elif case == "aniso":     # non-cubic volume, anisotropic voxels
+        r = ex1_renderer(vr.Volume(O.rand_volume(20)[:, :14, :9].copy(order="F")), res=res)
+        r.ElementSizeUm = [0.5, 1.0, 2.5]
+    elif case == "flat2d":    # 2-D emission volume (depth 1)
+        r = ex1_renderer(vr.Volume(O.rand_volume(16)[:, :, 0].copy(order="F")), res=res)
+    elif case == "onevoxel":
+        r = ex1_renderer(vr.Volume(np.float32(0.5)), res=res)
+    elif case == "nan":       # NaN voxels propagate identically
+        d = data.copy(order="F")
+        d[10:12, 10:12, 10:12] = np.nan
+        r = ex1_renderer(vr.Volume(d), res=res, lights=False)
+    r.render()
+    r.delete()
+
+
+def test_empty_image(counter_clock):
+    r = ex1_renderer(vr.Volume(O.shell_volume(16)), res=(0, 8), lights=False)
+    img = r.render()
+    assert img.shape == (8, 0, 3)
+    r.delete()
+
+
+def test_device_partitions_assemble_to_full_image(counter_clock):
+    """Image-space partition: parts rendered separately and assembled on the
+    device are bit-identical to the single full render; step counts add up."""
+    import torch
+    from volume_renderer_amd import mex
+    v = vr.Volume(O.shell_volume(40))
+    r = ex1_renderer(v, res=(123, 77))
+    full = r.render()
+    args = ("render", r.objectHandle, r.LightSources, r.VolumeIllumination,
+            np.float32([r.FactorEmission, r.FactorReflection, r.FactorAbsorption]), np.float32(r.ElementSizeUm),
+            np.uint64([77, 123]), np.flip(r.RotationMatrix, 0).astype(np.float32),
+            np.float32([0, r.FocalLength, r.DistanceToObject]), np.float32(r.OpacityThreshold), np.float32(r.Color))
+    ra, keep = mex.render_args(*args[2:])
+    W, H = 123, 77
+    for nparts, bc in ((1, 123), (2, 16), (3, 7), (8, 5)):
+        maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
+        parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
+        steps = torch.zeros(nparts, dtype=torch.int64, device="cuda")
+        for p in range(nparts):
+            mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts),
+                              steps[p:p + 1].data_ptr())
+        out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
+        mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
+        torch.cuda.synchronize()
+        img = out.cpu().numpy().reshape(-1)
+        assert np.array_equal(img.view(np.uint32), full.reshape(-1, order="F").view(np.uint32)), (nparts, bc)
+    r.delete()
+
+
+def test_step_count_matches_oracle(counter_clock):
+    import torch
+    from volume_renderer_amd import mex
+    v = vr.Volume(O.shell_volume(64))
+    r = ex1_renderer(v, res=(256, 256), lights=False)
+    r.render()
+    ra, keep = mex.render_args(False, False, np.float32([1, 0.4, 0.6]), np.float32([1, 1, 1]), np.uint64([256, 256]),
+                               np.flip(r.RotationMatrix, 0).astype(np.float32), np.float32([0, 3, 6]),
+                               np.float32(0.9), np.float32([1, 1, 0]))
+    out = torch.zeros(256 * 256 * 3, dtype=torch.float32, device="cuda")
+    steps = torch.zeros(1, dtype=torch.int64, device="cuda")
+    mex.render_device(r.objectHandle, ra, out.data_ptr(), None, steps.data_ptr())
+    torch.cuda.synchronize()
+    S = O.OracleSession()
+    h = S.new()
+    ov = O.OVolume(v.Data, 1)
+    S.sync_volumes(h, 0, ov, O.OVolume(np.ones((1, 1), np.float32), 1), ov)
+    _, total = S.render(h, None, None, [1, 0.4, 0.6], [1, 1, 1], [256, 256], np.flip(r.RotationMatrix, 0),
+                        [0, 3, 6], 0.9, [1, 1, 0])
+    assert abs(int(steps.item()) - total) <= total * 1e-4, (int(steps.item()), total)
+    r.delete()

@@ -1,0 +1,715 @@
+// vr_capi.hip -- host driver and C-ABI of libvrhip.so (declared in include/vrhip.h).
+//
+// Replaces, for the MI355X:
+//   - the mex command dispatcher /root/reference/src/C/mex/render.cpp:50-278 (marshalling kept)
+//   - the host render driver     /root/reference/src/C/vr/volumeRender.cpp:112-300
+//   - the persistent memory manager + handle /root/reference/src/C/vr/mm/mmanager.hxx,
+//     class_handle.hpp (same handle contract: signature check, dedup by (ptr, last_update, size))
+//   - the upload / texture-binding state machine /root/reference/src/C/vr/volumeRender_kernel.cu:
+//     600-867, re-expressed as host state: "textures" are bindings of device buffers (fp32 volumes
+//     resident in HBM, read by the software sampler of vr_kernels.hip), the slot indices d_idx* and
+//     the light list stay module-global exactly as in the reference.
+// Every HIP call is checked (the reference ignores errors in release builds, common.h:43-47).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/vrhip.h"
+#include "vr_device.h"
+
+namespace vr {
+hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, hipStream_t s);
+hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
+                           int64_t max_cols, float *out, hipStream_t s);
+hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s);
+}  // namespace vr
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+struct HipError {
+  hipError_t e;
+  const char *what;
+};
+
+#define VR_HIP(call)                                 \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) throw HipError{e_, #call}; \
+  } while (0)
+
+// texture ids = the reference's vr::VolumeType (volumeRender.h:149-157)
+enum TexId { T_EM = 0, T_AB = 1, T_RE = 2, T_DX = 3, T_DY = 4, T_DZ = 5, T_LIGHT = 6, T_COUNT = 7 };
+enum GradMethod { G_COMPUTE = 0, G_LOOKUP = 1 };
+
+// Host-side record of a MATLAB Volume (vr::Volume, volumeRender.h:61-70).
+struct VolRec {
+  const float *data = nullptr;
+  uint64_t dims[3] = {0, 0, 0};
+  uint64_t memory_size = 0;
+  uint64_t last_update = 0;
+  int32_t location = VR_HOST;
+};
+// operator== (volumeRender.cpp:24-26)
+bool same(const VolRec &a, const VolRec &b) {
+  return a.data == b.data && a.last_update == b.last_update && a.memory_size == b.memory_size;
+}
+
+VolRec make_rec(const vr_volume *v) {
+  VolRec r;
+  if (!v) return r;
+  r.data = v->data;
+  for (int i = 0; i < 3; ++i) r.dims[i] = v->dims[i];
+  r.memory_size = v->dims[0] * v->dims[1] * v->dims[2] * sizeof(float);
+  r.last_update = v->last_update;
+  r.location = v->location;
+  return r;
+}
+
+// A device-resident volume (the cudaArray analog): plain fp32, column-major, in HBM.
+struct DevBuf {
+  float *ptr = nullptr;
+  uint64_t dims[3] = {0, 0, 0};
+  uint64_t bytes = 0;
+  int device = 0;
+  ~DevBuf() {
+    if (ptr) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(device);
+      (void)hipFree(ptr);
+      (void)hipSetDevice(cur);
+    }
+  }
+};
+using BufPtr = std::shared_ptr<DevBuf>;
+
+}  // namespace
+
+// The MManager analog: per-handle last-synced volumes and their device buffers.
+struct vr_context {
+  uint32_t signature = 0xFF00F0A5u;  // class_handle.hpp:40
+  int device = 0;
+  uint64_t time_last_mem_sync = 0;
+  VolRec vol[T_COUNT];
+  BufPtr buf[T_COUNT];
+  float *d_out = nullptr;  // cached output buffer for the host-return path
+  size_t d_out_bytes = 0;
+};
+
+namespace {
+
+// Module-global device state of the reference (volumeRender_kernel.cu:49-120): texture bindings,
+// slot indices, gradient method, light list.  Shared by all handles, reset by 'delete'.
+struct TexUnit {
+  BufPtr bind[T_COUNT];
+  int32_t idx_em = T_EM, idx_ab = T_EM, idx_re = T_RE;  // kernel.cu:75-85
+  int32_t grad_method = G_COMPUTE;                       // kernel.cu:55
+  std::vector<vr::DevLight> lights;                      // c_numLightSources = lights.size()
+  vr::DevLight *d_lights = nullptr;
+  size_t d_lights_cap = 0;
+  int d_lights_device = 0;
+};
+
+std::mutex g_mu;
+TexUnit g_tex;
+std::set<vr_context *> g_contexts;
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) VR_HIP(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+void reset_tex_unit() {
+  for (auto &b : g_tex.bind) b.reset();
+  g_tex.idx_em = T_EM;
+  g_tex.idx_ab = T_EM;
+  g_tex.idx_re = T_RE;
+  g_tex.grad_method = G_COMPUTE;
+  g_tex.lights.clear();
+  if (g_tex.d_lights) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(g_tex.d_lights_device);
+    (void)hipFree(g_tex.d_lights);
+    (void)hipSetDevice(cur);
+  }
+  g_tex.d_lights = nullptr;
+  g_tex.d_lights_cap = 0;
+}
+
+bool valid(vr_context *h) { return h && g_contexts.count(h) && h->signature == 0xFF00F0A5u; }
+
+// syncVolume (kernel.cu:659-672): unbind the texture, drop the old array, upload the volume into a
+// fresh device buffer and bind it.  A buffer nobody else references is overwritten in place.
+void sync_volume(vr_context *h, int tex, int slot) {
+  g_tex.bind[tex].reset();
+  const VolRec &v = h->vol[slot];
+  BufPtr b = h->buf[slot];
+  if (!(b && b.use_count() == 1 && b->bytes == v.memory_size && b->device == h->device)) {
+    h->buf[slot].reset();
+    b = std::make_shared<DevBuf>();
+    b->device = h->device;
+    b->bytes = v.memory_size;
+    if (v.memory_size) VR_HIP(hipMalloc(&b->ptr, v.memory_size));
+  }
+  for (int i = 0; i < 3; ++i) b->dims[i] = v.dims[i];
+  if (v.memory_size) {
+    if (!v.data) throw HipError{hipErrorInvalidValue, "volume data is NULL"};
+    VR_HIP(hipMemcpy(b->ptr, v.data, v.memory_size,
+                     v.location == VR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+  }
+  h->buf[slot] = b;
+  g_tex.bind[tex] = b;
+}
+
+// The decisions of syncWithDevice (kernel.cu:739-867) over an abstract state, so that the real
+// state and vr_debug_slot_transition run the very same code.
+template <class S>
+void sync_decisions(S &s, bool simEmAb, bool simEmRe, bool simAbRe, bool reqEm, bool reqAb, bool reqRe) {
+  bool updEm = false, updAb = false, updRe = false;
+  if (reqEm) {
+    if (!updEm) { s.upload(T_EM); updEm = true; }
+    if (simEmRe && !updRe) { s.reference(T_RE, T_RE, &S::idx_re, T_EM); updRe = true; }
+    if (simEmAb && !updAb) { s.reference(T_AB, T_AB, &S::idx_ab, T_EM); updAb = true; }
+  }
+  if (reqAb) {
+    if (!updAb) { s.upload(T_AB); updAb = true; }
+    if (simAbRe && !updRe) { s.reference(T_RE, T_RE, &S::idx_re, T_AB); updRe = true; }
+    // kernel.cu:817-819 passes the absorption array for the emission texture (unreachable)
+    if (simEmAb && !updEm) { s.reference(T_EM, T_AB, &S::idx_em, T_AB); updEm = true; }
+  }
+  if (reqRe) {
+    if (!updRe) { s.upload(T_RE); updRe = true; }
+    if (simAbRe && !updAb) { s.reference(T_AB, T_AB, &S::idx_ab, T_RE); updAb = true; }
+    // kernel.cu:853-856: the "simEmAb" test guards Emission <- Reflection (reachable)
+    if (simEmAb && !updEm) { s.reference(T_EM, T_EM, &S::idx_em, T_RE); updEm = true; }
+  }
+}
+
+struct RealState {
+  vr_context *h;
+  int32_t idx_em, idx_ab, idx_re;  // shadow copies, written back after the decisions
+  void upload(int slot) { sync_volume(h, slot, slot); }
+  // referenceTexture (kernel.cu:631-648)
+  void reference(int tex, int bufslot, int32_t RealState::*idx, int target) {
+    if (h->buf[bufslot]) {
+      g_tex.bind[tex].reset();
+      h->buf[bufslot].reset();
+    }
+    this->*idx = target;
+  }
+};
+
+struct DebugState {
+  bool present[3] = {true, true, true};
+  bool bound[3] = {true, true, true};
+  int32_t idx_em, idx_ab, idx_re;
+  void upload(int slot) { present[slot] = true; bound[slot] = true; }
+  void reference(int tex, int bufslot, int32_t DebugState::*idx, int target) {
+    if (present[bufslot]) {
+      bound[tex] = false;
+      present[bufslot] = false;
+    }
+    this->*idx = target;
+  }
+};
+
+// MManager::getRequiredMemory (mmanager.hxx:110-133)
+uint64_t required_memory(const vr_context *h) {
+  const VolRec &em = h->vol[T_EM], &ab = h->vol[T_AB], &re = h->vol[T_RE];
+  uint64_t r = em.memory_size;
+  if (!same(em, ab) && !same(re, ab)) r += ab.memory_size;
+  if (!same(em, re) && !same(re, ab)) r += re.memory_size;
+  r += h->vol[T_DX].memory_size + h->vol[T_DY].memory_size + h->vol[T_DZ].memory_size;
+  return r;
+}
+
+// MManager::checkFreeDeviceMemory (mmanager.hxx:144-173)
+int check_free_device_memory(uint64_t required) {
+  size_t free_b = 0, total_b = 0;
+  VR_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (free_b >= required) return VR_OK;
+  std::ostringstream os;
+  os << "insufficient free VRAM!\n"
+     << "\tTotal Memory (MB): \t" << total_b / (1024 * 1024) << "\n"
+     << "\tFree Memory (MB): \t" << free_b / (1024 * 1024) << "\n"
+     << "\tRequired memory (MB): \t" << required / (1024 * 1024) << "\n";
+  return fail(VR_ERR_VRAM, os.str());
+}
+
+void reset_gradients(vr_context *h) {  // MManager::resetGradients (mmanager.hxx:206-213)
+  for (int s : {T_DX, T_DY, T_DZ}) {
+    h->buf[s].reset();
+    h->vol[s] = VolRec();
+  }
+}
+
+// MManager::sync (mmanager.hxx:178-201)
+void mm_sync(vr_context *h) {
+  if ((h->vol[T_DX].last_update == 0 && h->buf[T_DX]) || (h->vol[T_DY].last_update == 0 && h->buf[T_DY]) ||
+      (h->vol[T_DZ].last_update == 0 && h->buf[T_DZ]))
+    reset_gradients(h);
+  const VolRec &em = h->vol[T_EM], &ab = h->vol[T_AB], &re = h->vol[T_RE];
+  const uint64_t T = h->time_last_mem_sync;
+  RealState s{h, g_tex.idx_em, g_tex.idx_ab, g_tex.idx_re};
+  sync_decisions(s, same(em, ab), same(em, re), same(ab, re), em.last_update > T || T == 0,
+                 ab.last_update > T || T == 0, re.last_update > T || T == 0);
+  g_tex.idx_em = s.idx_em;
+  g_tex.idx_ab = s.idx_ab;
+  g_tex.idx_re = s.idx_re;
+  if (h->vol[T_DX].last_update != 0 && h->vol[T_DY].last_update != 0 && h->vol[T_DZ].last_update != 0) {
+    // setGradientTextures (kernel.cu:703-722): always re-uploads all three, then lookup mode
+    sync_volume(h, T_DX, T_DX);
+    sync_volume(h, T_DY, T_DY);
+    sync_volume(h, T_DZ, T_DZ);
+    g_tex.grad_method = G_LOOKUP;
+  }
+}
+
+vr::DevTex dev_tex(const BufPtr &b) {
+  vr::DevTex t{};
+  if (b && b->ptr) {
+    t.p = b->ptr;
+    t.nx = (int32_t)b->dims[0];
+    t.ny = (int32_t)b->dims[1];
+    t.nz = (int32_t)b->dims[2];
+  }
+  return t;
+}
+
+bool is_big(const vr::DevTex &t) {
+  return t.p && (uint64_t)t.nx * (uint64_t)t.ny * (uint64_t)t.nz > 0xFFFFFFFFull;
+}
+
+// initRender (volumeRender.cpp:112-156) + the per-frame constants of d_render.
+struct Frame {
+  vr::RenderParams P;
+  int mode = 0;
+  bool ab_alias = false, big = false;
+  bool degenerate = false;
+};
+
+int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
+  vr::RenderParams &P = F.P;
+  std::memset(&P, 0, sizeof(P));
+  const uint64_t H = a->resolution[0], W = a->resolution[1];
+  if (W > 0x7FFFFFFF || H > 0x7FFFFFFF || W * H > (1ull << 40))
+    return fail(VR_ERR_UNSUPPORTED, "image resolution too large");
+  P.width = (int32_t)W;
+  P.height = (int32_t)H;
+  P.fw = (float)W;
+  P.fh = (float)H;
+  P.ratio = (float)H / (float)W;
+  // factors = [Fe Fr Fa] -> initRender(..., Fe, Fr, Fa, ...)
+  P.fe = a->factors[0];
+  P.fr = a->factors[1];
+  P.fa = a->factors[2];
+  // element size reversed (make_float3Inv, render.cpp:35-37,195)
+  const float es[3] = {a->element_size_um[2], a->element_size_um[1], a->element_size_um[0]};
+  const VolRec &ev = h->vol[T_EM];  // extent of the handle's emission volume (render.cpp:245)
+  const uint64_t vw = ev.dims[0], vh = ev.dims[1], vd = ev.dims[2];
+  float bmax[3];
+  bmax[0] = 1.f;
+  bmax[1] = (es[1] * (float)vh) / ((float)vw * es[0]);
+  bmax[2] = (es[2] * (float)vd) / ((float)vw * es[0]);
+  for (int i = 0; i < 3; ++i) P.bmin[i] = -1.f * bmax[i];
+  const float dxy = sqrtf((float)(vw * vw + vh * vh));
+  const float dyz = sqrtf((float)(vh * vh + vd * vd));
+  const float dxz = sqrtf((float)(vw * vw + vd * vd));
+  const float mind = fminf(dxy, fminf(dyz, dxz));
+  P.tstep = 1.f / (2.2f * mind);
+  P.thr = a->opacity_threshold;
+  for (int i = 0; i < 3; ++i) {
+    P.bscale[i] = 1.f / (bmax[i] - P.bmin[i]);
+    P.color[i] = a->color[i];
+  }
+  P.gstep[0] = 1.f / (float)vw;  // volumeRender.cpp:273-275
+  P.gstep[1] = 1.f / (float)vh;
+  P.gstep[2] = 1.f / (float)vd;
+  // rotation: m[j] = column j of R, un-flipping MATLAB's flip(R) (render.cpp:211-221)
+  const float *r = a->rotation_flipped;
+  const float X[3] = {r[2], r[1], r[0]}, Y[3] = {r[5], r[4], r[3]}, Z[3] = {r[8], r[7], r[6]};
+  const float xoff = a->props[0], f = a->props[1], dist = a->props[2];
+  for (int i = 0; i < 3; ++i) {
+    P.eye[i] = fmaf(-dist, Z[i], xoff * X[i]);
+    P.ydir[i] = Y[i];
+    P.zdir[i] = Z[i];
+  }
+  const float xx = fmaf(X[2], X[2], fmaf(X[1], X[1], X[0] * X[0]));
+  const float xinv = 1.f / sqrtf(xx);
+  for (int i = 0; i < 3; ++i) P.nx_[i] = X[i] * xinv;
+  P.focal = f;
+  // textures through the slot indices (getTexture, kernel.cu:127-144)
+  P.em = dev_tex(g_tex.bind[g_tex.idx_em]);
+  P.ab = dev_tex(g_tex.bind[g_tex.idx_ab]);
+  P.re = dev_tex(g_tex.bind[g_tex.idx_re]);
+  P.gem = dev_tex(g_tex.bind[T_EM]);
+  P.gx = dev_tex(g_tex.bind[T_DX]);
+  P.gy = dev_tex(g_tex.bind[T_DY]);
+  P.gz = dev_tex(g_tex.bind[T_DZ]);
+  P.lut = dev_tex(g_tex.bind[T_LIGHT]);
+  P.num_lights = (int32_t)g_tex.lights.size();
+  P.lights = g_tex.d_lights;
+  F.mode = P.num_lights == 0 ? 0 : (g_tex.grad_method == G_LOOKUP ? 2 : 1);
+  F.ab_alias = P.ab.p == P.em.p && P.ab.nx == P.em.nx && P.ab.ny == P.em.ny && P.ab.nz == P.em.nz;
+  F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
+          is_big(P.gz);
+  if (is_big(P.lut)) return fail(VR_ERR_UNSUPPORTED, "illumination volume larger than 2^32 voxels");
+  bool finite = std::isfinite(P.tstep) && P.tstep > 0.f;
+  for (int i = 0; i < 3; ++i) finite = finite && std::isfinite(P.bmin[i]) && std::isfinite(P.bscale[i]);
+  // a sample-count cap every wave reaches: 2x the longest chord through the box in steps
+  const double diag = std::sqrt(4.0 * ((double)bmax[0] * bmax[0] + (double)bmax[1] * bmax[1] +
+                                       (double)bmax[2] * bmax[2]));
+  const double cap = 2.0 * diag / (double)P.tstep + 64.0;
+  P.max_steps = (finite && cap < 2.0e9) ? (int32_t)cap : 2000000000;
+  F.degenerate = !finite;  // no synced emission volume: nothing to march through (renders zeros)
+  return VR_OK;
+}
+
+// copyLightSources + setIlluminationTexture (render.cpp:145-191, kernel.cu:600-609,682-689)
+void upload_lights(vr_context *h, const vr_render_args *a) {
+  if (a->num_lights < 0 || !a->illumination) return;  // either argument is the logical false
+  const size_t n = (size_t)a->num_lights;
+  g_tex.lights.resize(n);
+  for (size_t l = 0; l < n; ++l) {
+    const vr_light &L = a->lights[l];
+    g_tex.lights[l] = vr::DevLight{L.position[2], L.position[1], L.position[0], L.color[0], L.color[1],
+                                   L.color[2]};
+  }
+  if (n > g_tex.d_lights_cap || g_tex.d_lights_device != h->device) {
+    if (g_tex.d_lights) (void)hipFree(g_tex.d_lights);
+    g_tex.d_lights = nullptr;
+    g_tex.d_lights_cap = 0;
+    VR_HIP(hipMalloc(&g_tex.d_lights, std::max<size_t>(n, 8) * sizeof(vr::DevLight)));
+    g_tex.d_lights_cap = std::max<size_t>(n, 8);
+    g_tex.d_lights_device = h->device;
+  }
+  if (n) VR_HIP(hipMemcpy(g_tex.d_lights, g_tex.lights.data(), n * sizeof(vr::DevLight), hipMemcpyHostToDevice));
+  h->vol[T_LIGHT] = make_rec(a->illumination);
+  sync_volume(h, T_LIGHT, T_LIGHT);
+}
+
+int64_t part_columns(int64_t w, int32_t bc, int32_t part, int32_t np) {
+  if (w <= 0) return 0;
+  if (np <= 1) return w;
+  const int64_t nblocks = (w + bc - 1) / bc;
+  int64_t cols = 0;
+  for (int64_t b = part; b < nblocks; b += np) cols += std::min<int64_t>(bc, w - b * bc);
+  return cols;
+}
+
+int validate_partition(const vr_partition *p) {
+  if (!p) return VR_OK;
+  if (p->num_parts < 1 || p->part < 0 || p->part >= p->num_parts || p->block_cols < 1)
+    return fail(VR_ERR_ARGUMENT, "invalid partition");
+  return VR_OK;
+}
+
+// The render command proper (render.cpp:134-259 minus the mxArray plumbing).
+int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
+              unsigned long long *d_steps, hipStream_t stream, Frame &F) {
+  if (a->num_lights > 0 && !a->lights) return fail(VR_ERR_ARGUMENT, "lights is NULL");
+  uint64_t required = required_memory(h);
+  if (a->num_lights >= 0 && a->illumination) {
+    required += a->illumination->dims[0] * a->illumination->dims[1] * a->illumination->dims[2] * 4 +
+                (uint64_t)a->num_lights * sizeof(vr::DevLight);
+    int rc = check_free_device_memory(required);
+    if (rc) return rc;
+  }
+  upload_lights(h, a);
+  required += a->resolution[0] * a->resolution[1] * sizeof(float) * 3;
+  int rc = check_free_device_memory(required);
+  if (rc) return rc;
+  rc = build_frame(h, a, F);
+  if (rc) return rc;
+  rc = validate_partition(part);
+  if (rc) return rc;
+  vr::RenderParams &P = F.P;
+  P.block_cols = part ? part->block_cols : std::max<int32_t>(P.width, 1);
+  P.part = part ? part->part : 0;
+  P.num_parts = part ? part->num_parts : 1;
+  P.part_cols = (int32_t)part_columns(P.width, P.block_cols, P.part, P.num_parts);
+  P.plane_cols = (int32_t)part_columns(P.width, P.block_cols, 0, P.num_parts);
+  P.out = d_out;
+  P.steps = d_steps;
+  const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
+  if (F.degenerate) {
+    if (out_bytes) VR_HIP(hipMemsetAsync(d_out, 0, out_bytes, stream));
+    return VR_OK;
+  }
+  VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, stream));
+  return VR_OK;
+}
+
+#define VR_GUARD_BEGIN try {
+#define VR_GUARD_END                                                                             \
+  }                                                                                              \
+  catch (const HipError &e) {                                                                    \
+    return fail(VR_ERR_DEVICE, std::string(hipGetErrorString(e.e)) + " in " + e.what);           \
+  }                                                                                              \
+  catch (const std::bad_alloc &) {                                                               \
+    return fail(VR_ERR_DEVICE, "host out of memory");                                            \
+  }
+
+double mb(uint64_t b) { return (double)b / (1024.0 * 1024.0); }
+
+}  // namespace
+
+extern "C" {
+
+int vr_new(vr_context **out) {
+  if (!out) return fail(VR_ERR_ARGUMENT, "New: One output expected.");
+  std::lock_guard<std::mutex> lk(g_mu);
+  VR_GUARD_BEGIN
+  int dev = 0;
+  VR_HIP(hipGetDevice(&dev));
+  vr_context *h = new vr_context();
+  h->device = dev;
+  g_contexts.insert(h);
+  *out = h;
+  g_last_error.clear();
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_delete(vr_context *h) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  VR_GUARD_BEGIN
+  // ~MManager -> cudaDeviceReset(): every handle's device memory and the module globals go.
+  reset_tex_unit();
+  for (vr_context *c : g_contexts) {
+    for (auto &b : c->buf) b.reset();
+    if (c->d_out) (void)hipFree(c->d_out);
+    c->d_out = nullptr;
+    c->d_out_bytes = 0;
+  }
+  g_contexts.erase(h);
+  h->signature = 0;
+  delete h;
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_mem_info(vr_context *h, char *buf, size_t buflen) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  size_t free_b = 0, total_b = 0;
+  VR_HIP(hipMemGetInfo(&free_b, &total_b));
+  const VolRec &em = h->vol[T_EM], &ab = h->vol[T_AB], &re = h->vol[T_RE];
+  auto ptr = [&](int s) { return (const void *)(h->buf[s] ? h->buf[s]->ptr : nullptr); };
+  std::ostringstream os;
+  os << "Memory Information\n"
+     << "------------------------------" << "last sync (timestamp): " << h->time_last_mem_sync << "\n\n"
+     << "\tGPU\n\t---\n"
+     << "\t\tTotal Memory (MB): \t" << mb(total_b) << "\n"
+     << "\t\tFree Memory (MB): \t" << mb(free_b) << "\n"
+     << "\t\tUsed Memory (MB): \t" << mb(total_b - free_b) << "\n\n"
+     << "\t\tVolumes\n\t\t-------\n"
+     << "\t\tEmission (MB): " << mb(em.memory_size) << " ptr: " << ptr(T_EM) << "\n"
+     << "\t\tAbsorption (MB): " << mb(ab.memory_size) << " ptr: " << ptr(T_AB) << "\n"
+     << "\t\tReflection (MB): " << mb(re.memory_size) << " ptr: " << ptr(T_RE) << "\n"
+     << "\t\tdX (MB): " << mb(h->vol[T_DX].memory_size) << " ptr: " << ptr(T_DX) << "\n"
+     << "\t\tdY (MB): " << mb(h->vol[T_DY].memory_size) << " ptr: " << ptr(T_DY) << "\n"
+     << "\t\tdZ (MB): " << mb(h->vol[T_DZ].memory_size) << " ptr: " << ptr(T_DZ) << "\n"
+     << "\t\tlight (MB): " << mb(h->vol[T_LIGHT].memory_size) << " ptr: " << ptr(T_LIGHT) << "\n\n"
+     << "\t\tSimilarity of Volumes\n\t\t---------------------\n"
+     << "\t\t\tEm\tAb\tRe\n"
+     << "\t\tEm\t1\t\n"
+     << "\t\tAb\t" << same(em, ab) << "\t1\n"
+     << "\t\tRe\t" << same(em, re) << "\t" << same(ab, re) << "\t1\n\n"
+     << "\t\tSlots (emission/absorption/reflection): " << g_tex.idx_em << " " << g_tex.idx_ab << " "
+     << g_tex.idx_re << ", gradient method: " << (g_tex.grad_method == G_LOOKUP ? "lookup" : "compute")
+     << ", lights: " << g_tex.lights.size() << "\n";
+  const std::string s = os.str();
+  if (buf && buflen) {
+    const size_t n = std::min(buflen - 1, s.size());
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume *emission,
+                    const vr_volume *reflection, const vr_volume *absorption, const vr_volume *dx,
+                    const vr_volume *dy, const vr_volume *dz) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!emission || !reflection || !absorption) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  const bool lookup = dx && dy && dz;
+  if (!lookup && (dx || dy || dz))
+    return fail(VR_ERR_ARGUMENT, "All gradient dimensions need to be set and of type Volume!");
+  for (const vr_volume *v : {emission, reflection, absorption, dx, dy, dz}) {
+    if (!v) continue;
+    const uint64_t n = v->dims[0] * v->dims[1] * v->dims[2];
+    if (n && !v->data) return fail(VR_ERR_ARGUMENT, "volume data is NULL");
+    if (v->dims[0] > 0x7FFFFFFF || v->dims[1] > 0x7FFFFFFF || v->dims[2] > 0x7FFFFFFF)
+      return fail(VR_ERR_UNSUPPORTED, "volume dimension too large");
+  }
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  uint64_t required = required_memory(h);  // render.cpp:90 (before the new volumes are recorded)
+  h->time_last_mem_sync = time_last_mem_sync;
+  h->vol[T_EM] = make_rec(emission);
+  h->vol[T_RE] = make_rec(reflection);
+  h->vol[T_AB] = make_rec(absorption);
+  if (lookup) {
+    h->vol[T_DX] = make_rec(dx);
+    h->vol[T_DY] = make_rec(dy);
+    h->vol[T_DZ] = make_rec(dz);
+  } else {
+    reset_gradients(h);
+  }
+  required += required_memory(h);
+  int rc = check_free_device_memory(required);
+  if (rc) return rc;
+  g_tex.grad_method = lookup ? G_LOOKUP : G_COMPUTE;  // setGradientMethod (render.cpp:121)
+  mm_sync(h);
+  VR_HIP(hipDeviceSynchronize());
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_render(vr_context *h, const vr_render_args *a, float *out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  const size_t bytes = (size_t)a->resolution[0] * (size_t)a->resolution[1] * 3 * sizeof(float);
+  if (bytes && !out) return fail(VR_ERR_ARGUMENT, "output is NULL");
+  if (bytes > h->d_out_bytes) {
+    if (h->d_out) VR_HIP(hipFree(h->d_out));
+    h->d_out = nullptr;
+    h->d_out_bytes = 0;
+    VR_HIP(hipMalloc(&h->d_out, bytes));
+    h->d_out_bytes = bytes;
+  }
+  Frame F;
+  int rc = do_render(h, a, nullptr, h->d_out, nullptr, nullptr, F);
+  if (rc) return rc;
+  if (bytes) VR_HIP(hipMemcpy(out, h->d_out, bytes, hipMemcpyDeviceToHost));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_render_device(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
+                     unsigned long long *d_steps, void *stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  Frame F;
+  return do_render(h, a, part, d_out, d_steps, (hipStream_t)stream, F);
+  VR_GUARD_END
+}
+
+int64_t vr_partition_columns(int64_t w, const vr_partition *p) {
+  if (!p) return w < 0 ? 0 : w;
+  if (p->num_parts < 1 || p->block_cols < 1 || p->part < 0 || p->part >= p->num_parts) return -1;
+  return part_columns(w, p->block_cols, p->part, p->num_parts);
+}
+
+int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t block_cols, int32_t num_parts,
+                           int64_t max_cols, float *d_out, void *stream) {
+  if (w < 0 || h < 0 || block_cols < 1 || num_parts < 1) return fail(VR_ERR_ARGUMENT, "invalid partition");
+  VR_GUARD_BEGIN
+  VR_HIP(vr::launch_assemble(d_parts, w, h, block_cols, num_parts, max_cols, d_out, (hipStream_t)stream));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_synth_shell_device(float *d_out, uint64_t n, void *stream) {
+  VR_GUARD_BEGIN
+  VR_HIP(vr::launch_synth_shell(d_out, n, (hipStream_t)stream));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_debug_slot_transition(const int32_t idx_in[3], int32_t sim_em_ab, int32_t sim_em_re, int32_t sim_ab_re,
+                             int32_t req_em, int32_t req_ab, int32_t req_re, int32_t idx_out[3],
+                             int32_t unbound_out[3]) {
+  DebugState s;
+  s.idx_em = idx_in[0];
+  s.idx_ab = idx_in[1];
+  s.idx_re = idx_in[2];
+  sync_decisions(s, sim_em_ab, sim_em_re, sim_ab_re, req_em, req_ab, req_re);
+  idx_out[0] = s.idx_em;
+  idx_out[1] = s.idx_ab;
+  idx_out[2] = s.idx_re;
+  for (int i = 0; i < 3; ++i) unbound_out[i] = !s.bound[i];
+  return VR_OK;
+}
+
+#define HG_PI ((float)3.141592653589793238462643383279502884197169399375105820)
+
+// HenyeyGreenstein.cc:39-91 (g in [-1, 1], value at c*N*N + a*N + b)
+int vr_henyey_greenstein(uint32_t n, float g, float *out) {
+  if (g > 1 || g < -1) return fail(VR_ERR_ARGUMENT, "g must be in interval [-1,1]");
+  if (n && !out) return fail(VR_ERR_ARGUMENT, "output is NULL");
+  const float frac_half = HG_PI / n;
+  const size_t page = (size_t)n * n;
+  const float num = 1.f - powf(g, 2.f);
+  const float g2 = powf(g, 2.f);
+  for (uint32_t c = 0; c < n; ++c) {
+    const float gamma = c * frac_half;
+    const float s = sinf(gamma), co = cosf(gamma);
+    for (uint32_t a = 0; a < n; ++a) {
+      const float alpha = a * frac_half;
+      const float lx = sinf(alpha), lz = cosf(alpha);
+      // lightOut (sin a, 0, cos a) rotated about X by gamma (float3.h:77-106)
+      const float rx = 1.f * lx + 0.f * 0.f + 0.f * lz;
+      const float ry = 0.f * lx + co * 0.f + s * lz;
+      const float rz = 0.f * lx + -s * 0.f + co * lz;
+      for (uint32_t b = 0; b < n; ++b) {
+        const float beta = b * frac_half;
+        const float ix = sinf(beta), iz = cosf(beta);
+        const float cosTheta = rx * ix + ry * 0.f + rz * iz;
+        const float den = sqrtf(powf((1.f + g2 - (2.f * g * cosTheta)), 3.f));
+        out[(size_t)c * page + (size_t)a * n + b] = 1.f / (4.f * HG_PI) * (num / den);
+      }
+    }
+  }
+  return VR_OK;
+}
+
+uint64_t vr_timestamp(void) {
+  const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                      std::chrono::system_clock::now().time_since_epoch())
+                      .count();
+  return (uint64_t)(uint32_t)(uint64_t)ms;  // stored through an int* (timestamp.cpp:25,33)
+}
+
+const char *vr_last_error(void) { return g_last_error.c_str(); }
+
+const char *vr_version(void) { return "libvrhip 0.1 gfx950 (MI355X) volume ray-marcher"; }
+
+}  // extern "C"

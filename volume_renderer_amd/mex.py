@@ -1,0 +1,247 @@
+"""The three MEX entry points of the reference, re-exposed over libvrhip's C-ABI.
+
+``volumeRender(cmd, ...)`` keeps the command protocol and the argument marshalling of
+/root/reference/src/C/mex/render.cpp:50-278 (positional MATLAB arguments, same order, same
+permutations -- done inside libvrhip exactly where the reference does them), ``HenyeyGreenstein``
+mirrors /root/reference/src/C/mex/HenyeyGreenstein.cc:29-96 and ``timestamp`` mirrors
+/root/reference/src/C/mex/timestamp.cpp:17-33.  MATLAB values map to Python as:
+logical ``false`` -> ``False``; ``single``/``uint64`` arrays -> numpy arrays (column-major);
+``Volume``/``LightSource`` objects -> the classes of this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import warnings
+
+import numpy as np
+
+from . import _lib
+from ._lib import VrLight, VrRenderArgs, VrVolume, check, lib
+
+_clock = None
+
+
+def set_clock(fn) -> None:
+    """Replace the millisecond clock behind ``timestamp`` (tests use a deterministic counter;
+    the reference's change tracking misses updates made within the same millisecond,
+    SURVEY.md A.9).  ``None`` restores the real clock."""
+    global _clock
+    _clock = fn
+
+
+def timestamp() -> np.uint64:
+    """ms since the epoch, low 32 bits (timestamp.cpp stores it through an int*)."""
+    if _clock is not None:
+        return np.uint64(_clock())
+    return np.uint64(lib().vr_timestamp())
+
+
+def HenyeyGreenstein(n, g=0.8) -> np.ndarray:
+    """N x N x N single LUT of the Henyey-Greenstein phase function (HenyeyGreenstein.cc)."""
+    n = int(n)
+    out = np.empty((n, n, n), dtype=np.float32, order="F")
+    check(lib().vr_henyey_greenstein(ctypes.c_uint32(n), ctypes.c_float(g), out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+def _is_false(x) -> bool:
+    return isinstance(x, (bool, np.bool_)) and not bool(x)
+
+
+def _matlab_dims(a: np.ndarray):
+    """mxGetDimensions as the mex reads them: (d0, d1, d2) with d2 = 1 for 2-D data."""
+    if a.ndim == 0:
+        return (1, 1, 1)
+    if a.ndim == 1:
+        return (a.shape[0], 1, 1)
+    if a.ndim == 2:
+        return (a.shape[0], a.shape[1], 1)
+    if a.ndim == 3:
+        return tuple(a.shape)
+    raise ValueError("volumes must have at most 3 dimensions")
+
+
+class DeviceVolume:
+    """A Volume whose Data already lives in HBM (e.g. a torch tensor on cuda): MATLAB-shaped dims
+    (d0, d1, d2), column-major fp32 at device address `ptr`.  Synced device-to-device."""
+
+    def __init__(self, ptr: int, dims, last_update=None, owner=None):
+        self.ptr = int(ptr)
+        d = tuple(int(x) for x in dims) + (1,) * (3 - len(dims))
+        self.dims = d[:3]
+        self.TimeLastUpdate = timestamp() if last_update is None else np.uint64(last_update)
+        self.owner = owner  # keeps the backing allocation alive
+
+    @classmethod
+    def from_tensor(cls, t, dims=None, last_update=None):
+        """`t` is a contiguous float32 cuda tensor holding the column-major data."""
+        import torch
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise TypeError("DeviceVolume needs a contiguous float32 cuda tensor")
+        dims = dims if dims is not None else tuple(reversed(t.shape))  # C-order (z,y,x) tensor -> (x,y,z)
+        return cls(t.data_ptr(), dims, last_update, owner=t)
+
+    def min(self):
+        return 0.0
+
+
+def _vr_volume(vol) -> VrVolume:
+    """mxMake_volume (volumeRender.cpp:307-342): zero-copy view of Data + TimeLastUpdate."""
+    v = VrVolume()
+    if isinstance(vol, DeviceVolume):
+        v.data = vol.ptr
+        for i in range(3):
+            v.dims[i] = vol.dims[i]
+        v.last_update = int(vol.TimeLastUpdate)
+        v.location = _lib.VR_DEVICE
+        return v
+    data = vol.Data
+    if not (isinstance(data, np.ndarray) and data.dtype == np.float32 and
+            (data.flags.f_contiguous or data.ndim <= 1)):
+        raise TypeError("Volume.Data must be a column-major single array")
+    v.data = data.ctypes.data if data.size else None
+    d = _matlab_dims(data)
+    for i in range(3):
+        v.dims[i] = d[i]
+    v.last_update = int(vol.TimeLastUpdate)
+    v.location = _lib.VR_HOST
+    return v
+
+
+def _handle(h) -> ctypes.c_void_p:
+    a = np.asarray(h)
+    if a.size != 1 or a.dtype != np.uint64:
+        raise _lib.VrError(_lib.VR_OK + 1, "Input must be a real uint64 scalar.")
+    return ctypes.c_void_p(int(a.reshape(-1)[0]))
+
+
+def _f32(x, n: int, name: str) -> np.ndarray:
+    a = np.asarray(x, dtype=np.float32).reshape(-1, order="F")
+    if a.size < n:
+        raise ValueError(f"{name}: expected {n} values")
+    return a
+
+
+def render_args(lights_arg, illum_arg, factors, element_size_um, resolution, rotation_flipped, props,
+                opacity_threshold, color):
+    """Marshal the positional 'render' arguments (prhs[2..10], render.cpp:142-240) into the
+    C-ABI struct.  Returns (VrRenderArgs, keep-alive list)."""
+    ra = VrRenderArgs()
+    keep = []
+    if not (_is_false(lights_arg) or _is_false(illum_arg)):
+        lights = list(lights_arg) if isinstance(lights_arg, (list, tuple, np.ndarray)) else [lights_arg]
+        arr = (VrLight * max(len(lights), 1))()
+        for i, ls in enumerate(lights):
+            pos = _f32(ls.Position, 3, "Position")
+            col = _f32(ls.Color, 3, "Color")
+            for k in range(3):
+                arr[i].position[k] = pos[k]
+                arr[i].color[k] = col[k]
+        illum = _vr_volume(illum_arg)
+        keep += [arr, illum, getattr(illum_arg, "Data", None)]
+        ra.lights = ctypes.cast(arr, ctypes.POINTER(VrLight))
+        ra.num_lights = len(lights)
+        ra.illumination = ctypes.pointer(illum)
+    else:
+        ra.num_lights = -1
+        ra.illumination = None
+    fac = _f32(factors, 3, "factors")
+    es = _f32(element_size_um, 3, "ElementSizeUm")
+    res = np.asarray(resolution).reshape(-1)
+    rot = _f32(rotation_flipped, 9, "RotationMatrix")
+    pr = _f32(props, 3, "props")
+    thr = np.float32(np.asarray(opacity_threshold).reshape(-1)[0])
+    col = _f32(color, 3, "Color")
+    for k in range(3):
+        ra.factors[k] = fac[k]
+        ra.element_size_um[k] = es[k]
+        ra.props[k] = pr[k]
+        ra.color[k] = col[k]
+    for k in range(9):
+        ra.rotation_flipped[k] = rot[k]
+    ra.resolution[0] = int(res[0])
+    ra.resolution[1] = int(res[1])
+    ra.opacity_threshold = thr
+    return ra, keep
+
+
+def partition(block_cols: int, part: int, num_parts: int) -> _lib.VrPartition:
+    p = _lib.VrPartition()
+    p.block_cols, p.part, p.num_parts = int(block_cols), int(part), int(num_parts)
+    return p
+
+
+def partition_columns(width: int, part) -> int:
+    return int(lib().vr_partition_columns(int(width), ctypes.byref(part) if part is not None else None))
+
+
+def render_device(handle, ra: VrRenderArgs, d_out: int, part=None, d_steps: int = 0, stream: int = 0) -> None:
+    """'render' into device memory (vr_render_device): asynchronous on `stream`."""
+    check(lib().vr_render_device(_handle(handle), ctypes.byref(ra), ctypes.byref(part) if part is not None else None,
+                                 ctypes.c_void_p(int(d_out)), ctypes.c_void_p(int(d_steps)) if d_steps else None,
+                                 ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def assemble_partitions(d_parts: int, width: int, height: int, block_cols: int, num_parts: int, max_cols: int,
+                        d_out: int, stream: int = 0) -> None:
+    check(lib().vr_assemble_partitions(ctypes.c_void_p(int(d_parts)), int(width), int(height), int(block_cols),
+                                       int(num_parts), int(max_cols), ctypes.c_void_p(int(d_out)),
+                                       ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def synth_shell_device(d_out: int, n: int, stream: int = 0) -> None:
+    check(lib().vr_synth_shell_device(ctypes.c_void_p(int(d_out)), int(n),
+                                      ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def volumeRender(cmd, *args):
+    """The `volumeRender` mex: commands 'new', 'delete', 'mem_info', 'sync_volumes', 'render'."""
+    nrhs = 1 + len(args)
+    if not isinstance(cmd, str) or len(cmd) >= 64:
+        raise _lib.VrError(1, "First input should be a command string less than 64 characters long.")
+    L = lib()
+    if cmd == "new":
+        p = ctypes.c_void_p()
+        check(L.vr_new(ctypes.byref(p)))
+        return np.uint64(p.value)
+    if nrhs < 2:
+        raise _lib.VrError(1, "Second input should be a class instance handle.")
+    h = _handle(args[0])
+    if cmd == "delete":
+        check(L.vr_delete(h))
+        if nrhs != 2:
+            warnings.warn("Delete: Unexpected arguments ignored.")
+        return None
+    if cmd == "mem_info":
+        buf = ctypes.create_string_buffer(1 << 14)
+        check(L.vr_mem_info(h, buf, len(buf)))
+        print(buf.value.decode(), end="")
+        return None
+    if cmd == "sync_volumes":
+        if nrhs < 6:
+            raise _lib.VrError(1, "insufficient parameter!")
+        t_sync = int(np.asarray(args[1]).reshape(-1)[0])
+        em, re, ab = (_vr_volume(v) for v in args[2:5])  # order: Emission, Reflection, Absorption
+        if nrhs == 9:
+            gx, gy, gz = (_vr_volume(v) for v in args[5:8])
+            check(L.vr_sync_volumes(h, t_sync, ctypes.byref(em), ctypes.byref(re), ctypes.byref(ab),
+                                    ctypes.byref(gx), ctypes.byref(gy), ctypes.byref(gz)))
+        elif nrhs == 6:
+            check(L.vr_sync_volumes(h, t_sync, ctypes.byref(em), ctypes.byref(re), ctypes.byref(ab),
+                                    None, None, None))
+        else:
+            raise _lib.VrError(5, "sync_volumes: expected 6 or 9 arguments")
+        if nrhs > 9:
+            warnings.warn("SyncVolumes: Unexpected arguments ignored.")
+        return None
+    if cmd == "render":
+        if nrhs < 11:
+            raise _lib.VrError(1, "insufficient parameter!")
+        ra, keep = render_args(*args[1:10])
+        res = np.asarray(args[5]).reshape(-1)
+        H, W = int(res[0]), int(res[1])
+        out = np.zeros((H, W, 3), dtype=np.float32, order="F")
+        check(L.vr_render(h, ctypes.byref(ra), out.ctypes.data_as(ctypes.c_void_p) if out.size else None))
+        del keep
+        return out
+    return None

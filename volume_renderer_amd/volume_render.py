@@ -1,0 +1,231 @@
+"""Python mirror of the reference's MATLAB class ``VolumeRender`` and enum ``StereoRenderMode``.
+
+/root/reference/src/matlab/VolumeRender/VolumeRender.m and StereoRenderMode.m.  Property names,
+defaults, validation, the `render` / `p_render` call sequence (sync_volumes then render, stereo as
+two full renders) and the argument marshalling into the `volumeRender` mex are kept one for one, so
+that code written against the MATLAB API translates line by line.  Images are numpy arrays of
+shape [H, W, 3] (column-major float32, like MATLAB single).
+"""
+from __future__ import annotations
+
+import enum
+import math
+import warnings
+
+import numpy as np
+
+from .mex import timestamp, volumeRender
+from .volume import LightSource, Volume
+
+
+class StereoRenderMode(enum.Enum):
+    RedCyan = 0
+    LeftRightHorizontal = 1
+
+
+def _is_logical(x) -> bool:
+    return isinstance(x, (bool, np.bool_))
+
+
+def _sind(a: float) -> float:
+    """MATLAB sind: exact at integer multiples of 90 degrees."""
+    a = float(a)
+    r = math.fmod(a, 360.0)
+    if r == int(r) and int(r) % 90 == 0:
+        return [0.0, 1.0, 0.0, -1.0][(int(r) // 90) % 4]
+    return math.sin(math.radians(a))
+
+
+def _cosd(a: float) -> float:
+    a = float(a)
+    r = math.fmod(a, 360.0)
+    if r == int(r) and int(r) % 90 == 0:
+        return [1.0, 0.0, -1.0, 0.0][(int(r) // 90) % 4]
+    return math.cos(math.radians(a))
+
+
+_VOLUME_PROPS = ("VolumeEmission", "VolumeAbsorption", "VolumeReflection", "VolumeGradientX",
+                 "VolumeGradientY", "VolumeGradientZ", "VolumeIllumination")
+
+
+class VolumeRender:
+    """Renderer handle; see VolumeRender.m:1-62 for the property documentation."""
+
+    # the MATLAB default VolumeReflection = Volume(1) is created once per class load and shared
+    _default_reflection = None
+
+    def __init__(self, *varargin):
+        object.__setattr__(self, "objectHandle", None)
+        self.FocalLength = 0.0
+        self.DistanceToObject = 0.0
+        self.OpacityThreshold = 0.95
+        self.LightSources = False
+        self.Color = np.array([1.0, 1.0, 1.0])
+        self.FactorEmission = 1.0
+        self.FactorReflection = 1.0
+        self.FactorAbsorption = 1.0
+        self.CameraXOffset = 0.0
+        self.StereoOutput = StereoRenderMode.RedCyan
+        self.ElementSizeUm = np.array([1.0, 1.0, 1.0])
+        self.RotationMatrix = np.eye(3)
+        self.ImageResolution = np.array([0, 0])
+        self.TimeLastMemSync = np.uint64(0)
+        if VolumeRender._default_reflection is None:
+            VolumeRender._default_reflection = Volume(1)
+        # observable properties: defaults are assigned without firing the listener
+        object.__setattr__(self, "VolumeReflection", VolumeRender._default_reflection)
+        for p in _VOLUME_PROPS:
+            if p != "VolumeReflection":
+                object.__setattr__(self, p, False)
+        object.__setattr__(self, "objectHandle", volumeRender("new", *varargin))
+
+    # -- property validation + PostSet listener (VolumeRender.m:349-493, 723-740) --------------
+    def __setattr__(self, name, val):
+        if name == "LightSources":
+            if not _is_logical(val):
+                seq = val if isinstance(val, (list, tuple)) else [val]
+                if not all(isinstance(v, LightSource) for v in seq):
+                    raise TypeError("LightSources must be a 1xN vector with data of type LightSource!")
+                val = list(seq)
+        elif name in ("VolumeIllumination", "VolumeEmission", "VolumeReflection", "VolumeAbsorption"):
+            if not isinstance(val, Volume):
+                raise TypeError(f"{'VolumeEmission' if name == 'VolumeIllumination' else name} must be of type Volume")
+            if name == "VolumeAbsorption" and val.min() < 0:
+                warnings.warn("VolumeAbsorption is not allowed to contain data smaller than 0!")
+        elif name in ("VolumeGradientX", "VolumeGradientY", "VolumeGradientZ"):
+            if not (isinstance(val, Volume) or (_is_logical(val) and not val)):
+                raise TypeError(f"{name} must be of type Volume")
+        elif name in ("Color", "ElementSizeUm"):
+            val = np.asarray(val, dtype=np.float64).reshape(3)
+        elif name == "ImageResolution":
+            val = np.asarray(val, dtype=np.float64).reshape(2)
+        elif name == "RotationMatrix":
+            val = np.asarray(val, dtype=np.float64).reshape(3, 3)
+        object.__setattr__(self, name, val)
+        if name in _VOLUME_PROPS and isinstance(val, Volume):
+            val.TimeLastUpdate = timestamp()
+
+    def __del__(self):
+        h = getattr(self, "objectHandle", None)
+        if h is not None:
+            try:
+                volumeRender("delete", h)
+            except Exception:
+                pass
+            object.__setattr__(self, "objectHandle", None)
+
+    def delete(self) -> None:
+        self.__del__()
+
+    def syncVolumes(self) -> None:
+        """VolumeRender.m:188-219."""
+        grads = [self.VolumeGradientX, self.VolumeGradientY, self.VolumeGradientZ]
+        if not any(_is_logical(g) for g in grads):
+            volumeRender("sync_volumes", self.objectHandle, self.TimeLastMemSync, self.VolumeEmission,
+                         self.VolumeReflection, self.VolumeAbsorption, *grads)
+        else:
+            volumeRender("sync_volumes", self.objectHandle, self.TimeLastMemSync, self.VolumeEmission,
+                         self.VolumeReflection, self.VolumeAbsorption)
+        self.TimeLastMemSync = timestamp()
+
+    def memInfo(self) -> None:
+        volumeRender("mem_info", self.objectHandle)
+
+    def memClear(self) -> None:
+        volumeRender("delete", self.objectHandle)
+        object.__setattr__(self, "objectHandle", None)
+
+    def rotate(self, alpha, beta, gamma) -> None:
+        """RotationMatrix = RotationMatrix * Rx(alpha) * Ry(beta) * Rz(gamma), degrees (:239-262)."""
+        ca, sa, cb, sb, cg, sg = _cosd(alpha), _sind(alpha), _cosd(beta), _sind(beta), _cosd(gamma), _sind(gamma)
+        rx = np.array([[1, 0, 0], [0, ca, -sa], [0, sa, ca]], dtype=np.float64)
+        ry = np.array([[cb, 0, sb], [0, 1, 0], [-sb, 0, cb]], dtype=np.float64)
+        rz = np.array([[cg, -sg, 0], [sg, cg, 0], [0, 0, 1]], dtype=np.float64)
+        self.RotationMatrix = self.RotationMatrix @ rx @ ry @ rz
+
+    def resetGradientVolumes(self) -> None:
+        self.VolumeGradientX = False
+        self.VolumeGradientY = False
+        self.VolumeGradientZ = False
+
+    def render(self) -> np.ndarray:
+        """VolumeRender.m:264-309: mono render, or off-axis stereo composed from two renders."""
+        res = np.flip(self.ImageResolution)  # [H W]
+        if self.CameraXOffset == 0:
+            return self._p_render(np.float32(self.CameraXOffset), res)
+        base = self.CameraXOffset / 2
+        fov = 2 * math.atan(1 / self.FocalLength)
+        delta = base * self.ImageResolution[1] / (2 * self.FocalLength * math.tan(fov / 2))
+        delta = int(math.floor(abs(delta) + 0.5)) * (1 if delta >= 0 else -1)  # MATLAB round
+        resolution = res + np.array([0, delta])
+        right = self._p_render(base, resolution)
+        left = self._p_render(-base, resolution)
+        left = _imcrop(left, delta + 1, left.shape[1])
+        right = _imcrop(right, 0, right.shape[1] - delta)
+        if self.StereoOutput == StereoRenderMode.RedCyan:
+            img = np.zeros((left.shape[0], left.shape[1], 3), dtype=np.float64, order="F")
+            img[:, :, 0] = left[:, :, 0]
+            img[:, :, 1] = right[:, :, 1]
+            img[:, :, 2] = right[:, :, 2]
+            return img
+        return np.asfortranarray(np.concatenate([left, right], axis=1))
+
+    def _p_render(self, camera_x_offset, resolution) -> np.ndarray:
+        """VolumeRender.m:497-583."""
+        validate = [_is_logical(self.VolumeReflection), _is_logical(self.VolumeAbsorption),
+                    _is_logical(self.VolumeEmission)]
+        if _is_logical(self.VolumeIllumination):
+            warnings.warn("VolumeIllumination is unset. Thus no lightning will be applied!")
+        if any(validate):
+            raise ValueError("Not all volumes are properly set!")
+        grads = [self.VolumeGradientX, self.VolumeGradientY, self.VolumeGradientZ]
+        with_grads = False
+        if not any(_is_logical(g) for g in grads):
+            if not all(isinstance(g, Volume) for g in grads):
+                raise ValueError("All gradient dimensions need to be set and of type Volume!")
+            with_grads = True
+        self.syncVolumes()
+        factors = np.array([self.FactorEmission, self.FactorReflection, self.FactorAbsorption])
+        props = np.array([camera_x_offset, self.FocalLength, self.DistanceToObject], dtype=np.float64)
+        matrix = np.flip(self.RotationMatrix, axis=0)
+        args = ["render", self.objectHandle, self.LightSources, self.VolumeIllumination,
+                factors.astype(np.float32), self.ElementSizeUm.astype(np.float32),
+                np.asarray(resolution).astype(np.uint64), matrix.astype(np.float32),
+                props.astype(np.float32), np.float32(self.OpacityThreshold), self.Color.astype(np.float32)]
+        if with_grads:
+            args += grads
+        return volumeRender(*args)
+
+    # -- static helpers (VolumeRender.m:587-701) ------------------------------------------------
+    @staticmethod
+    def normalizeSequence(sequence) -> np.ndarray:
+        s = np.asarray(sequence, dtype=np.float64)
+        if s.ndim < 4:
+            raise ValueError("input must be a multiframe image (4D)")
+        mx, mn = s.max(), s.min()
+        out = np.zeros_like(s)
+        for i in range(s.shape[3]):
+            out[:, :, :, i] = VolumeRender.normalizeImage(s[:, :, :, i], mn, mx)
+        return out
+
+    @staticmethod
+    def normalizeImage(image_rgb, *varargin) -> np.ndarray:
+        img = np.asarray(image_rgb, dtype=np.float64)
+        r, g, b = img[:, :, 0], img[:, :, 1], img[:, :, 2]
+        mn = min(r.min(), g.min(), b.min()) if len(varargin) < 1 else varargin[0]
+        mx = max(r.max(), g.max(), b.max()) if len(varargin) < 2 else varargin[1]
+        if mn < 0:
+            r, g, b = r + mn, g + mn, b + mn
+            mx = mx + abs(mn)
+        out = np.zeros(img.shape)
+        out[:, :, 0], out[:, :, 1], out[:, :, 2] = r / mx, g / mx, b / mx
+        return out
+
+
+def _imcrop(img: np.ndarray, xmin: float, width: float) -> np.ndarray:
+    """imcrop(img, [xmin 0 width H]) as VolumeRender.render uses it: columns round(xmin) ..
+    round(xmin + width), clamped to the image, all rows."""
+    n = img.shape[1]
+    c1 = max(int(math.floor(xmin + 0.5)), 1)
+    c2 = min(int(math.floor(xmin + width + 0.5)), n)
+    return img[:, c1 - 1:c2, :]
