@@ -100,12 +100,13 @@ def main():
     full = torch.zeros(3 * W * H, dtype=torch.float32, device=dev) if rank == 0 else None
     gathered = (torch.zeros(world * 3 * max_cols * H, dtype=torch.float32, device=dev)
                 if (world > 1 and rank == 0) else None)
-    steps_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    steps_t = torch.zeros(2, dtype=torch.int64, device=dev)
 
     # sample count of this rank's launch (exact, counter variant; untimed)
     mex.render_device(h, ra, out_local.data_ptr(), part, steps_t.data_ptr(), sptr)
     torch.cuda.synchronize(dev)
-    my_samples = int(steps_t.item())
+    my_samples = int(steps_t[0].item())
+    my_lit = int(steps_t[1].item())
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
@@ -138,13 +139,14 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
 
-    samples_all = torch.tensor([my_samples], dtype=torch.int64, device=dev)
+    samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(samples_all, op=dist.ReduceOp.SUM)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    total_samples = int(samples_all.item())
+    total_samples = int(samples_all[0].item())
+    total_lit = int(samples_all[1].item())
 
     result = None
     if rank == 0:
@@ -174,6 +176,7 @@ def main():
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else "")},
             "samples_per_frame": total_samples,
+            "shaded_samples_per_frame": total_lit,
             "gb_per_s_sample_stream": round(4.0 * total_samples * F / (elapsed / args.steps) / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

@@ -119,7 +119,8 @@ uint64_t vr_timestamp(void);
 
 /* 'render' without the host round trip: writes the (partitioned, if part != NULL) image to the
  * device buffer d_out on `stream` (a hipStream_t; NULL = default stream).  Asynchronous.
- * If d_steps != NULL, the total number of ray-march samples is atomically added to *d_steps. */
+ * If d_steps != NULL it points to two counters: d_steps[0] += ray-march samples taken,
+ * d_steps[1] += samples that evaluated gradient + shading (the others had opacity exactly 0). */
 int vr_render_device(vr_context *h, const vr_render_args *args, const vr_partition *part,
                      float *d_out, unsigned long long *d_steps, void *stream);
 

@@ -65,6 +65,12 @@ def assert_parity(got: np.ndarray, ref32: np.ndarray, ref64: np.ndarray, what: s
     frac = float(ok.mean()) if ok.size else 1.0
     stats = dict(max_abs=float(d.max()) if d.size else 0.0, scale=scale, frac_within=frac,
                  bit_exact=float((got.view(np.uint32) == ref32.view(np.uint32)).mean()) if got.size else 1.0)
+    bad = (frac < 0.999) or (stats["max_abs"] > 1e-2 * scale)
+    if bad and os.environ.get("PARITY_DUMP"):
+        os.makedirs(os.environ["PARITY_DUMP"], exist_ok=True)
+        name = "".join(ch if ch.isalnum() else "_" for ch in (os.environ.get("PYTEST_CURRENT_TEST", "") + what))
+        np.savez_compressed(os.path.join(os.environ["PARITY_DUMP"], name[-120:] + ".npz"),
+                            got=got, ref32=ref32, ref64=ref64)
     assert frac >= 0.999, f"{what}: only {frac:.5f} within envelope; {stats}"
     assert stats["max_abs"] <= 1e-2 * scale, f"{what}: max |d| {stats['max_abs']} > 1e-2*max; {stats}"
     return stats

@@ -240,10 +240,10 @@ def test_device_partitions_assemble_to_full_image(counter_clock):
     for nparts, bc in ((1, 123), (2, 16), (3, 7), (8, 5)):
         maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
         parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
-        steps = torch.zeros(nparts, dtype=torch.int64, device="cuda")
+        steps = torch.zeros((nparts, 2), dtype=torch.int64, device="cuda")
         for p in range(nparts):
             mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts),
-                              steps[p:p + 1].data_ptr())
+                              steps[p].data_ptr())
         out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
         mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
         torch.cuda.synchronize()
@@ -262,7 +262,7 @@ def test_step_count_matches_oracle(counter_clock):
                                np.flip(r.RotationMatrix, 0).astype(np.float32), np.float32([0, 3, 6]),
                                np.float32(0.9), np.float32([1, 1, 0]))
     out = torch.zeros(256 * 256 * 3, dtype=torch.float32, device="cuda")
-    steps = torch.zeros(1, dtype=torch.int64, device="cuda")
+    steps = torch.zeros(2, dtype=torch.int64, device="cuda")
     mex.render_device(r.objectHandle, ra, out.data_ptr(), None, steps.data_ptr())
     torch.cuda.synchronize()
     S = O.OracleSession()
@@ -271,5 +271,5 @@ def test_step_count_matches_oracle(counter_clock):
     S.sync_volumes(h, 0, ov, O.OVolume(np.ones((1, 1), np.float32), 1), ov)
     _, total = S.render(h, None, None, [1, 0.4, 0.6], [1, 1, 1], [256, 256], np.flip(r.RotationMatrix, 0),
                         [0, 3, 6], 0.9, [1, 1, 0])
-    assert abs(int(steps.item()) - total) <= total * 1e-4, (int(steps.item()), total)
+    assert abs(int(steps[0].item()) - total) <= total * 1e-4, (int(steps[0].item()), total)
     r.delete()

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -28,7 +29,9 @@
 #include "vr_device.h"
 
 namespace vr {
-hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, hipStream_t s);
+hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
+hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
+hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
 hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s);
@@ -82,12 +85,15 @@ VolRec make_rec(const vr_volume *v) {
   return r;
 }
 
-// A device-resident volume (the cudaArray analog): plain fp32, column-major, in HBM.
+// A device-resident volume (the cudaArray analog): fp32 in HBM in the apron layout of
+// vr_device.h ((d0+2) x (d1+2) x (d2+2), edge-replicated border), plus its upload statistics.
 struct DevBuf {
   float *ptr = nullptr;
   uint64_t dims[3] = {0, 0, 0};
-  uint64_t bytes = 0;
+  uint64_t bytes = 0;  // padded allocation size
   int device = 0;
+  bool nonfinite = false;
+  float maxabs = 0.f;
   ~DevBuf() {
     if (ptr) {
       int cur = 0;
@@ -168,19 +174,44 @@ bool valid(vr_context *h) { return h && g_contexts.count(h) && h->signature == 0
 void sync_volume(vr_context *h, int tex, int slot) {
   g_tex.bind[tex].reset();
   const VolRec &v = h->vol[slot];
+  const uint64_t n = v.dims[0] * v.dims[1] * v.dims[2];
+  const uint64_t padded = n ? (v.dims[0] + 2) * (v.dims[1] + 2) * (v.dims[2] + 2) * sizeof(float) : 0;
   BufPtr b = h->buf[slot];
-  if (!(b && b.use_count() == 1 && b->bytes == v.memory_size && b->device == h->device)) {
+  if (!(b && b.use_count() == 1 && b->bytes == padded && b->device == h->device)) {
     h->buf[slot].reset();
     b = std::make_shared<DevBuf>();
     b->device = h->device;
-    b->bytes = v.memory_size;
-    if (v.memory_size) VR_HIP(hipMalloc(&b->ptr, v.memory_size));
+    b->bytes = padded;
+    if (padded) VR_HIP(hipMalloc(&b->ptr, padded));
   }
   for (int i = 0; i < 3; ++i) b->dims[i] = v.dims[i];
-  if (v.memory_size) {
+  b->nonfinite = false;
+  b->maxabs = 0.f;
+  if (n) {
     if (!v.data) throw HipError{hipErrorInvalidValue, "volume data is NULL"};
-    VR_HIP(hipMemcpy(b->ptr, v.data, v.memory_size,
-                     v.location == VR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    const float *src = v.data;
+    float *staging = nullptr;
+    if (v.location != VR_DEVICE) {  // H2D into a dense staging buffer, then pad on the device
+      VR_HIP(hipMalloc(&staging, n * sizeof(float)));
+      hipError_t e = hipMemcpy(staging, v.data, n * sizeof(float), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        (void)hipFree(staging);
+        throw HipError{e, "hipMemcpy (volume upload)"};
+      }
+      src = staging;
+    }
+    vr::BufStats *d_st = nullptr;
+    vr::BufStats st{0u, 0.f};
+    hipError_t e = hipMalloc(&d_st, sizeof(vr::BufStats));
+    if (e == hipSuccess) e = hipMemset(d_st, 0, sizeof(vr::BufStats));
+    if (e == hipSuccess) e = vr::launch_pad(src, b->ptr, (int32_t)v.dims[0], (int32_t)v.dims[1], (int32_t)v.dims[2], nullptr);
+    if (e == hipSuccess) e = vr::launch_stats(src, n, d_st, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(&st, d_st, sizeof(st), hipMemcpyDeviceToHost);
+    if (staging) (void)hipFree(staging);
+    if (d_st) (void)hipFree(d_st);
+    if (e != hipSuccess) throw HipError{e, "volume upload (pad/stats)"};
+    b->nonfinite = st.nonfinite != 0;
+    b->maxabs = st.maxabs;
   }
   h->buf[slot] = b;
   g_tex.bind[tex] = b;
@@ -297,19 +328,35 @@ vr::DevTex dev_tex(const BufPtr &b) {
     t.nx = (int32_t)b->dims[0];
     t.ny = (int32_t)b->dims[1];
     t.nz = (int32_t)b->dims[2];
+    t.px = (uint32_t)(b->dims[0] + 2);
+    t.pxy = (uint32_t)((b->dims[0] + 2) * (b->dims[1] + 2));
+    t.fnx = (float)t.nx;
+    t.fny = (float)t.ny;
+    t.fnz = (float)t.nz;
+    t.one = (t.nx == 1 && t.ny == 1 && t.nz == 1);
   }
   return t;
 }
 
 bool is_big(const vr::DevTex &t) {
-  return t.p && (uint64_t)t.nx * (uint64_t)t.ny * (uint64_t)t.nz > 0xFFFFFFFFull;
+  return t.p && ((uint64_t)t.nx + 2) * ((uint64_t)t.ny + 2) * ((uint64_t)t.nz + 2) > 0xFFFFFFFFull;
 }
+
+bool same_tex(const vr::DevTex &a, const vr::DevTex &b) {
+  return a.p == b.p && a.nx == b.nx && a.ny == b.ny && a.nz == b.nz;
+}
+bool same_dims(const vr::DevTex &a, const vr::DevTex &b) {
+  return a.nx == b.nx && a.ny == b.ny && a.nz == b.nz;
+}
+
+// finite and comfortably below FLT_MAX (a texture that is unbound reads 0)
+bool tame(const BufPtr &b) { return !b || !b->ptr || (!b->nonfinite && b->maxabs < 1e30f); }
 
 // initRender (volumeRender.cpp:112-156) + the per-frame constants of d_render.
 struct Frame {
   vr::RenderParams P;
   int mode = 0;
-  bool ab_alias = false, big = false;
+  bool ab_alias = false, big = false, share = false;
   bool degenerate = false;
 };
 
@@ -375,7 +422,39 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
   P.num_lights = (int32_t)g_tex.lights.size();
   P.lights = g_tex.d_lights;
   F.mode = P.num_lights == 0 ? 0 : (g_tex.grad_method == G_LOOKUP ? 2 : 1);
-  F.ab_alias = P.ab.p == P.em.p && P.ab.nx == P.em.nx && P.ab.ny == P.em.ny && P.ab.nz == P.em.nz;
+  F.ab_alias = same_tex(P.ab, P.em);
+  const bool em_grid = P.em.p && !P.em.one;  // the centre sample computes its three axes
+  if (F.mode == 1)
+    F.share = em_grid && same_tex(P.gem, P.em);
+  else if (F.mode == 2)
+    F.share = em_grid && P.gx.p && P.gy.p && P.gz.p && !P.gx.one && same_dims(P.gx, P.em) &&
+              same_dims(P.gy, P.em) && same_dims(P.gz, P.em);
+  P.re_is_em = same_tex(P.re, P.em) && P.em.p != nullptr;
+  // Empty-sample skip: a sample with alpha == 0 adds fma(eds, c, ill) * 0 to the
+  // sum; that is exactly +-0 (a no-op) whenever the illumination term `ill` is finite, which holds
+  // if the reflection texture, the LUT, the light colours, the colour and Fr are finite and small.
+  {
+    const BufPtr &rb = g_tex.bind[g_tex.idx_re];
+    const BufPtr &lb = g_tex.bind[T_LIGHT];
+    bool ok = tame(rb) && tame(lb) && std::isfinite(P.fr) && std::fabs(P.fr) < 1e3f;
+    double bound = 1.0;
+    for (int i = 0; i < 3; ++i) {
+      ok = ok && std::isfinite(P.color[i]) && std::fabs(P.color[i]) < 1e3f;
+      bound = std::max(bound, (double)std::fabs(P.color[i]));
+    }
+    double lmax = 0.0;
+    for (const auto &L : g_tex.lights) {
+      for (float c : {L.cr, L.cg, L.cb}) {
+        ok = ok && std::isfinite(c);
+        lmax = std::max(lmax, (double)std::fabs(c));
+      }
+    }
+    const double rmax = (rb && rb->ptr) ? rb->maxabs : 0.0, lutmax = (lb && lb->ptr) ? lb->maxabs : 0.0;
+    ok = ok && (double)std::fabs(P.fr) * rmax * lutmax * lmax * bound * (double)(g_tex.lights.size() + 1) < 1e36;
+    P.skip_empty = ok ? 1 : 0;
+    if (const char *ev = std::getenv("VR_NO_EMPTY_SKIP"))  // A/B switch for measurements
+      if (ev[0] == '1') P.skip_empty = 0;
+  }
   F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
           is_big(P.gz);
   if (is_big(P.lut)) return fail(VR_ERR_UNSUPPORTED, "illumination volume larger than 2^32 voxels");
@@ -461,7 +540,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     if (out_bytes) VR_HIP(hipMemsetAsync(d_out, 0, out_bytes, stream));
     return VR_OK;
   }
-  VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, stream));
+  VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
   return VR_OK;
 }
 

@@ -5,12 +5,20 @@
 
 namespace vr {
 
-// A bound "texture": fp32 volume in HBM, column-major, x (d0) fastest.  p == nullptr means the
-// texture reference is unbound and reads 0 (the reference's unbound tex3D).
+// A bound "texture": an fp32 volume resident in HBM in the apron layout of DESIGN.md s5 -- the
+// logical nx*ny*nz column-major volume (x fastest) surrounded by a one-voxel border that
+// replicates the edge voxels, i.e. P[k][j][i] = T[clamp(k-1)][clamp(j-1)][clamp(i-1)] for
+// i in [0, nx+1] etc.  With it the clamp-addressed tap pair (clamp(i), clamp(i+1)) of the linear
+// filter is always the contiguous pair P[i'+1], P[i'+2] with i' = clamp(i, -1, n-1): one 8-byte
+// load per row, no per-tap clamping.  p == nullptr means the texture reference is unbound and
+// reads 0.
 struct DevTex {
   const float *p;
   int32_t nx, ny, nz;
-  int32_t pad_;
+  uint32_t px;    // nx + 2 (row pitch, elements)
+  uint32_t pxy;   // (nx + 2) * (ny + 2) (plane pitch, elements)
+  float fnx, fny, fnz;  // (float)n for the coordinate transform
+  int32_t one;    // 1x1x1 volume: every fetch is the single voxel
 };
 
 // One light in kernel order (position reversed from MATLAB, render.cpp:167-168).
@@ -41,11 +49,20 @@ struct RenderParams {
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
+  int32_t re_is_em;               // reflection texture == emission texture (sample reused)
+  int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   // image-space partition (vr_partition): local column lc -> global column
   int32_t block_cols, part, num_parts, part_cols;
   int32_t plane_cols;             // column stride of the output planes (part 0's column count)
   float *out;                     // [3][plane_cols][H]: column-major planar image of the part
   unsigned long long *steps;      // optional sample counter
+};
+
+// Per-buffer statistics computed on the device at upload (used to prove the empty-sample skip
+// exact): any non-finite voxel, and the largest magnitude.
+struct BufStats {
+  uint32_t nonfinite;
+  float maxabs;
 };
 
 }  // namespace vr

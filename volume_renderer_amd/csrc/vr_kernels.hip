@@ -4,9 +4,20 @@
 // 16x16 pixels.  Front-to-back emission/absorption compositing with early ray termination,
 // software trilinear sampling with the CUDA linear-filter semantics of the reference's tex3D
 // (/root/reference/src/C/vr/volumeRender_kernel.cu:544-548), on-the-fly (:212-253) or lookup
-// (:266-276) gradient, Henyey-Greenstein LUT shading per light (:308-353).  The arithmetic follows
-// the contract of DESIGN.md s4 op for op (explicit fmaf, -ffp-contract=off) so that the HIP path and
-// the CPU oracle (oracle/vr_oracle.c) agree to the last bit wherever libm's expf/acosf do.
+// (:266-276) gradient, Henyey-Greenstein LUT shading per light (:308-353).
+//
+// Numerics: the ray set-up, the march recurrences (t += tstep, pos += step), the
+// sample coordinates, the 8-bit filter weights and the lerps follow the oracle op for op (explicit
+// fmaf, -ffp-contract=off), so sample positions and texel fetches are bit-identical to the oracle.
+// Shading (normalize, lengths, angles) is the oracle's op sequence with correctly rounded
+// sqrt/div; only expf/acosf come from the device math library (<= 1 ulp from glibc).
+//
+// Memory: volumes live in the apron layout of vr_device.h, so every trilinear fetch
+// is 4 x global_load_dwordx2 (one per (y,z) row of the 2x2x2 cell) with no per-tap clamping; the
+// six gradient taps reuse the centre sample's weights on the two unshifted axes; a 1x1x1 texture
+// (the class default VolumeReflection = Volume(1)) is one scalar load.  Samples whose opacity is
+// exactly 0 contribute exactly 0 and skip gradient+shading when the host has proven every other
+// term finite (skip_empty).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -16,61 +27,84 @@
 namespace vr {
 
 #define VR_PI ((float)3.14159265358979323846f)  // volumeRender_kernel.cu:20
+#define VR_INV_PI 0.318309886183790671538f
 
 struct f3 {
   float x, y, z;
 };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-__device__ __forceinline__ float len3(f3 a) { return sqrtf(dot3(a, a)); }
-__device__ __forceinline__ float angle3(f3 a, f3 b) {
-  return acosf(dot3(a, b) / (len3(a) * len3(b)));
+
+typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+// acos(x) / pi for x in [-1, 1] (NaN outside, like acosf): A&S 4.4.46, |err| <= 2e-8 + rounding
+__device__ __forceinline__ float acos_over_pi(float x) {
+  const float a = fabsf(x);
+  float p = -0.0012624911f;
+  p = fmaf(p, a, 0.0066700901f);
+  p = fmaf(p, a, -0.0170881256f);
+  p = fmaf(p, a, 0.0308918810f);
+  p = fmaf(p, a, -0.0501743046f);
+  p = fmaf(p, a, 0.0889789874f);
+  p = fmaf(p, a, -0.2145988016f);
+  p = fmaf(p, a, 1.5707963050f);
+  const float r = __builtin_amdgcn_sqrtf(1.f - a) * p * VR_INV_PI;  // acos(|x|)/pi
+  return x < 0.f ? 1.f - r : r;
 }
 
-// One axis of the linear-filter address computation (normalized coords, clamp addressing).
-__device__ __forceinline__ float tex_axis(float c, int n, int &i0, int &i1) {
+// One axis of the linear-filter address computation (normalized coords, clamp addressing):
+// pair base i' = clamp(floor(c*n - 0.5), -1, n-1) and the 8-bit weight.
+struct Ax {
+  int i;
+  float w;
+};
+__device__ __forceinline__ Ax axis(float c, int n, float fn) {
   c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
-  const float xb = c * (float)n - 0.5f;
+  const float xb = c * fn - 0.5f;
   const float fl = floorf(xb);
   const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
   const int i = (int)fl;
-  i0 = min(max(i, 0), n - 1);
-  i1 = min(max(i + 1, 0), n - 1);
-  return w;
+  return Ax{min(max(i, -1), n - 1), w};
 }
 
 __device__ __forceinline__ float lerp(float a, float b, float w) { return fmaf(w, b - a, a); }
 
+// Trilinear fetch from the apron layout given the three axes.
+template <bool BIG>
+__device__ __forceinline__ float fetch(const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
+  const float *b;
+  if (BIG) {
+    const uint64_t o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
+    b = t.p + o;
+  } else {
+    const uint32_t o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
+    b = t.p + o;
+  }
+  const f2a4 r00 = *reinterpret_cast<const f2a4 *>(b);
+  const f2a4 r10 = *reinterpret_cast<const f2a4 *>(b + t.px);
+  const f2a4 r01 = *reinterpret_cast<const f2a4 *>(b + t.pxy);
+  const f2a4 r11 = *reinterpret_cast<const f2a4 *>(b + t.pxy + t.px);
+  const float c00 = lerp(r00.x, r00.y, ax.w), c10 = lerp(r10.x, r10.y, ax.w);
+  const float c01 = lerp(r01.x, r01.y, ax.w), c11 = lerp(r11.x, r11.y, ax.w);
+  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
+  return lerp(c0, c1, az.w);
+}
+
+// tex3D on any texture state (unbound -> 0, 1x1x1 -> single voxel through the same lerp algebra).
 template <bool BIG>
 __device__ __forceinline__ float tex3d(const DevTex &t, float x, float y, float z) {
-  if (t.p == nullptr) return 0.f;  // unbound texture reads 0 (wave-uniform branch)
-  int x0, x1, y0, y1, z0, z1;
-  const float wx = tex_axis(x, t.nx, x0, x1);
-  const float wy = tex_axis(y, t.ny, y0, y1);
-  const float wz = tex_axis(z, t.nz, z0, z1);
-  const float *p = t.p;
-  float v[8];
-  if (BIG) {
-    const uint64_t sy = (uint64_t)t.nx, sz = (uint64_t)t.nx * (uint64_t)t.ny;
-    const uint64_t r00 = y0 * sy + z0 * sz, r10 = y1 * sy + z0 * sz;
-    const uint64_t r01 = y0 * sy + z1 * sz, r11 = y1 * sy + z1 * sz;
-    v[0] = p[r00 + x0]; v[1] = p[r00 + x1]; v[2] = p[r10 + x0]; v[3] = p[r10 + x1];
-    v[4] = p[r01 + x0]; v[5] = p[r01 + x1]; v[6] = p[r11 + x0]; v[7] = p[r11 + x1];
-  } else {
-    const uint32_t sy = (uint32_t)t.nx, sz = (uint32_t)t.nx * (uint32_t)t.ny;
-    const uint32_t r00 = y0 * sy + z0 * sz, r10 = y1 * sy + z0 * sz;
-    const uint32_t r01 = y0 * sy + z1 * sz, r11 = y1 * sy + z1 * sz;
-    v[0] = p[r00 + x0]; v[1] = p[r00 + x1]; v[2] = p[r10 + x0]; v[3] = p[r10 + x1];
-    v[4] = p[r01 + x0]; v[5] = p[r01 + x1]; v[6] = p[r11 + x0]; v[7] = p[r11 + x1];
+  if (t.p == nullptr) return 0.f;  // wave-uniform
+  if (t.one) {
+    const float v = t.p[0];
+    return fmaf(0.5f, v - v, v);  // == lerp(v, v, w) for every w (NaN/inf/-0 included)
   }
-  const float c00 = lerp(v[0], v[1], wx), c10 = lerp(v[2], v[3], wx);
-  const float c01 = lerp(v[4], v[5], wx), c11 = lerp(v[6], v[7], wx);
-  const float c0 = lerp(c00, c10, wy), c1 = lerp(c01, c11, wy);
-  return lerp(c0, c1, wz);
+  return fetch<BIG>(t, axis(x, t.nx, t.fnx), axis(y, t.ny, t.fny), axis(z, t.nz, t.fnz));
 }
 
 // MODE 0: no light sources (shade() contributes exactly 0); 1: on-the-fly gradient; 2: lookup.
-template <int MODE, bool AB_ALIAS, bool BIG, bool COUNT>
+// SHARE: the gradient texture(s) have the emission texture's dims, so the unshifted axes of the
+// gradient taps (MODE 1) / all axes of the lookups (MODE 2) are the centre sample's.
+template <int MODE, bool AB_ALIAS, bool BIG, bool COUNT, bool SHARE>
 __global__ __launch_bounds__(256) void render_kernel(const RenderParams P) {
   // 16x16 pixel workgroup tile; wave w owns the 8x8 quadrant (w & 1, w >> 1); lane -> (x, y)
   // with y fastest so that the column-major output stores of a lane octet are contiguous.
@@ -78,7 +112,7 @@ __global__ __launch_bounds__(256) void render_kernel(const RenderParams P) {
   const int lc = blockIdx.x * 16 + (wave & 1) * 8 + (lane >> 3);  // local (partition) column
   const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane & 7);
   const bool active = (lc < P.part_cols) && (y < P.height);
-  int32_t nsteps = 0;
+  int32_t nsteps = 0, nlit = 0;
   if (active) {
     const int blk = lc / P.block_cols, within = lc - blk * P.block_cols;
     const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
@@ -122,14 +156,31 @@ __global__ __launch_bounds__(256) void render_kernel(const RenderParams P) {
       float t = tnear;
       for (;;) {
         const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
-        const float em_s = tex3d<BIG>(P.em, ps.x, ps.y, ps.z);
+        // centre sample (emission slot; absorption aliases it unless the slots differ)
+        float em_s = 0.f;
+        Ax ax{0, 0.f}, ay{0, 0.f}, az{0, 0.f};
+        if (P.em.p != nullptr) {
+          if (P.em.one) {
+            const float q = P.em.p[0];
+            em_s = fmaf(0.5f, q - q, q);
+          } else {
+            ax = axis(ps.x, P.em.nx, P.em.fnx);
+            ay = axis(ps.y, P.em.ny, P.em.fny);
+            az = axis(ps.z, P.em.nz, P.em.fnz);
+            em_s = fetch<BIG>(P.em, ax, ay, az);
+          }
+        }
         const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
         const float e = P.fe * em_s;
         const float a = P.fa * ab_s;
         const float alpha = 1.f - expf(-a * tstep);
         const float eds = e * tstep;
         float ir = 0.f, ig = 0.f, ib = 0.f;
-        if (MODE != 0) {
+        // opacity exactly 0 and a finite emission term: the sample adds exactly 0 (every other
+        // term is finite by the host's scan), so gradient and shading are skipped.
+        const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
+        if (MODE != 0 && !skip) {
+          if (COUNT) ++nlit;
           f3 g;
           if (MODE == 1) {
             const float xp = ((pos.x + P.gstep[0]) - bmin.x) * bsc.x;
@@ -138,31 +189,55 @@ __global__ __launch_bounds__(256) void render_kernel(const RenderParams P) {
             const float ym = ((pos.y - P.gstep[1]) - bmin.y) * bsc.y;
             const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
             const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
-            g.x = tex3d<BIG>(P.gem, xp, ps.y, ps.z) - tex3d<BIG>(P.gem, xm, ps.y, ps.z);
-            g.y = tex3d<BIG>(P.gem, ps.x, yp, ps.z) - tex3d<BIG>(P.gem, ps.x, ym, ps.z);
-            g.z = tex3d<BIG>(P.gem, ps.x, ps.y, zp) - tex3d<BIG>(P.gem, ps.x, ps.y, zm);
+            if (SHARE) {  // gem == em: reuse the centre's axes on the unshifted coordinates
+              const DevTex &T = P.gem;
+              g.x = fetch<BIG>(T, axis(xp, T.nx, T.fnx), ay, az) - fetch<BIG>(T, axis(xm, T.nx, T.fnx), ay, az);
+              g.y = fetch<BIG>(T, ax, axis(yp, T.ny, T.fny), az) - fetch<BIG>(T, ax, axis(ym, T.ny, T.fny), az);
+              g.z = fetch<BIG>(T, ax, ay, axis(zp, T.nz, T.fnz)) - fetch<BIG>(T, ax, ay, axis(zm, T.nz, T.fnz));
+            } else {
+              g.x = tex3d<BIG>(P.gem, xp, ps.y, ps.z) - tex3d<BIG>(P.gem, xm, ps.y, ps.z);
+              g.y = tex3d<BIG>(P.gem, ps.x, yp, ps.z) - tex3d<BIG>(P.gem, ps.x, ym, ps.z);
+              g.z = tex3d<BIG>(P.gem, ps.x, ps.y, zp) - tex3d<BIG>(P.gem, ps.x, ps.y, zm);
+            }
             g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
           } else {
-            g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
-                   tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
+            if (SHARE)
+              g = mk(fetch<BIG>(P.gx, ax, ay, az), fetch<BIG>(P.gy, ax, ay, az), fetch<BIG>(P.gz, ax, ay, az));
+            else
+              g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
+                     tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
           }
+          // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
+          // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n
+          // below cancel when the view ray is parallel to n, and gamma then depends on every bit
+          // of n (an rsq here moved whole pixels by ~1%).
           const float ginv = 1.f / sqrtf(dot3(g, g));
           const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
-          const float refl = P.fr * tex3d<BIG>(P.re, ps.x, ps.y, ps.z);
-          const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
-          const float nlen = len3(n), lilen = len3(li);
-          const float alpha_n = acosf(dot3(n, li) / (nlen * lilen)) / VR_PI;
+          const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
+          const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
+          // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle
+          const float nlen = sqrtf(dot3(n, n));
+          const float alpha_n = acosf(dot3(n, li) / (nlen * sqrtf(dot3(li, li)))) / VR_PI;
           const float dli = dot3(li, n);
           const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-          const float liplen = len3(lip);
+          const float liplen = sqrtf(dot3(lip, lip));
+          const Ax la = axis(alpha_n, P.lut.nx, P.lut.fnx);
           for (int i = 0; i < P.num_lights; ++i) {
             const DevLight L = P.lights[i];
-            const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
-            const float beta = acosf(dot3(n, lo) / (nlen * len3(lo))) / VR_PI;
+            const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);  // lightOut
+            const float beta = acosf(dot3(n, lo) / (nlen * sqrtf(dot3(lo, lo)))) / VR_PI;
             const float dlo = dot3(lo, n);
             const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-            const float gamma = acosf(dot3(lip, lop) / (liplen * len3(lop))) / VR_PI;
-            const float light = tex3d<false>(P.lut, alpha_n, beta, gamma);
+            const float gamma = acosf(dot3(lip, lop) / (liplen * sqrtf(dot3(lop, lop)))) / VR_PI;
+            float light = 0.f;
+            if (P.lut.p != nullptr) {
+              if (P.lut.one) {
+                const float q = P.lut.p[0];
+                light = fmaf(0.5f, q - q, q);
+              } else {
+                light = fetch<false>(P.lut, la, axis(beta, P.lut.ny, P.lut.fny), axis(gamma, P.lut.nz, P.lut.fnz));
+              }
+            }
             const float rl = refl * light;
             ir = fmaf(rl * L.cr, P.color[0], ir);
             ig = fmaf(rl * L.cg, P.color[1], ig);
@@ -193,11 +268,15 @@ __global__ __launch_bounds__(256) void render_kernel(const RenderParams P) {
     P.out[k + plane] = sg;
     P.out[k + 2 * plane] = sb;
   }
-  if (COUNT) {
-    unsigned long long s = (unsigned long long)nsteps;
+  if (COUNT) {  // steps[0] += samples, steps[1] += samples that ran gradient + shading
+    unsigned long long s = (unsigned long long)nsteps, l = (unsigned long long)nlit;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_xor(s, off, 64);
+      l += __shfl_xor(l, off, 64);
+    }
     if (lane == 0 && s) atomicAdd(P.steps, s);
+    if (lane == 0 && l) atomicAdd(P.steps + 1, l);
   }
 }
 
@@ -243,31 +322,82 @@ __global__ __launch_bounds__(256) void synth_shell_kernel(float *__restrict__ ou
   }
 }
 
+// ---- upload into the apron layout ------------------------------------------------------------
+
+// Copy a dense column-major nx*ny*nz volume into the padded buffer, writing the replicated apron in
+// the same pass: padded voxel (i, j, k) = T[clamp(i-1)][clamp(j-1)][clamp(k-1)].
+__global__ __launch_bounds__(256) void pad_volume_kernel(const float *__restrict__ src, float *__restrict__ dst,
+                                                         int32_t nx, int32_t ny, int32_t nz) {
+  const uint64_t px = (uint64_t)nx + 2, py = (uint64_t)ny + 2, pz = (uint64_t)nz + 2;
+  const uint64_t total = px * py * pz;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < total;
+       q += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = q % px, r = q / px, j = r % py, k = r / py;
+    const uint64_t si = i == 0 ? 0 : (i > (uint64_t)nx ? (uint64_t)nx - 1 : i - 1);
+    const uint64_t sj = j == 0 ? 0 : (j > (uint64_t)ny ? (uint64_t)ny - 1 : j - 1);
+    const uint64_t sk = k == 0 ? 0 : (k > (uint64_t)nz ? (uint64_t)nz - 1 : k - 1);
+    dst[q] = src[(sk * (uint64_t)ny + sj) * (uint64_t)nx + si];
+  }
+}
+
+// nonfinite flag and max |x| of a dense buffer (one atomic pair per workgroup)
+__global__ __launch_bounds__(256) void stats_kernel(const float *__restrict__ src, uint64_t n, BufStats *st) {
+  uint32_t bad = 0;
+  float mx = 0.f;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
+    const float v = src[q];
+    if (!(fabsf(v) <= 3.4028234e38f)) bad = 1;
+    else mx = fmaxf(mx, fabsf(v));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    bad |= __shfl_xor(bad, off, 64);
+    mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+  }
+  __shared__ uint32_t sb[4];
+  __shared__ float sm[4];
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = bad;
+    sm[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t bb = sb[0] | sb[1] | sb[2] | sb[3];
+    const float m = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    if (bb) atomicOr(&st->nonfinite, 1u);
+    atomicMax(reinterpret_cast<unsigned int *>(&st->maxabs), __float_as_uint(m));  // m >= 0
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launch helpers (called from vr_capi.hip)
 
-template <int MODE, bool AB, bool BIG>
-static hipError_t launch3(const RenderParams &P, dim3 grid, hipStream_t s) {
+template <int MODE, bool AB, bool BIG, bool SH>
+static hipError_t launch4(const RenderParams &P, dim3 grid, hipStream_t s) {
   if (P.steps)
-    hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, true>), grid, dim3(256), 0, s, P);
+    hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, true, SH>), grid, dim3(256), 0, s, P);
   else
-    hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, false>), grid, dim3(256), 0, s, P);
+    hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, false, SH>), grid, dim3(256), 0, s, P);
   return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t launch2(const RenderParams &P, bool ab_alias, bool big, dim3 grid, hipStream_t s) {
-  if (ab_alias) return big ? launch3<MODE, true, true>(P, grid, s) : launch3<MODE, true, false>(P, grid, s);
-  return big ? launch3<MODE, false, true>(P, grid, s) : launch3<MODE, false, false>(P, grid, s);
+template <int MODE, bool AB>
+static hipError_t launch3(const RenderParams &P, bool big, bool share, dim3 grid, hipStream_t s) {
+  if (big) return share ? launch4<MODE, AB, true, true>(P, grid, s) : launch4<MODE, AB, true, false>(P, grid, s);
+  return share ? launch4<MODE, AB, false, true>(P, grid, s) : launch4<MODE, AB, false, false>(P, grid, s);
 }
 
-hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, hipStream_t s) {
+template <int MODE>
+static hipError_t launch2(const RenderParams &P, bool ab_alias, bool big, bool share, dim3 grid, hipStream_t s) {
+  return ab_alias ? launch3<MODE, true>(P, big, share, grid, s) : launch3<MODE, false>(P, big, share, grid, s);
+}
+
+hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s) {
   if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
   dim3 grid((unsigned)((P.part_cols + 15) / 16), (unsigned)((P.height + 15) / 16));
   switch (mode) {
-    case 0: return launch2<0>(P, ab_alias, big, grid, s);
-    case 1: return launch2<1>(P, ab_alias, big, grid, s);
-    default: return launch2<2>(P, ab_alias, big, grid, s);
+    case 0: return launch2<0>(P, ab_alias, big, false, grid, s);
+    case 1: return launch2<1>(P, ab_alias, big, share, grid, s);
+    default: return launch2<2>(P, ab_alias, big, share, grid, s);
   }
 }
 
@@ -288,6 +418,22 @@ hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s) {
   uint64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(synth_shell_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s) {
+  const uint64_t total = ((uint64_t)nx + 2) * ((uint64_t)ny + 2) * ((uint64_t)nz + 2);
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(pad_volume_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, nx, ny, nz);
+  return hipGetLastError();
+}
+
+hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s) {
+  if (!n) return hipSuccess;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(stats_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, n, st);
   return hipGetLastError();
 }
 
