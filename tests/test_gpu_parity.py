@@ -240,7 +240,7 @@ def test_device_partitions_assemble_to_full_image(counter_clock):
     for nparts, bc in ((1, 123), (2, 16), (3, 7), (8, 5)):
         maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
         parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
-        steps = torch.zeros((nparts, 2), dtype=torch.int64, device="cuda")
+        steps = torch.zeros((nparts, 5), dtype=torch.int64, device="cuda")
         for p in range(nparts):
             mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts),
                               steps[p].data_ptr())
@@ -262,7 +262,7 @@ def test_step_count_matches_oracle(counter_clock):
                                np.flip(r.RotationMatrix, 0).astype(np.float32), np.float32([0, 3, 6]),
                                np.float32(0.9), np.float32([1, 1, 0]))
     out = torch.zeros(256 * 256 * 3, dtype=torch.float32, device="cuda")
-    steps = torch.zeros(2, dtype=torch.int64, device="cuda")
+    steps = torch.zeros(5, dtype=torch.int64, device="cuda")
     mex.render_device(r.objectHandle, ra, out.data_ptr(), None, steps.data_ptr())
     torch.cuda.synchronize()
     S = O.OracleSession()
@@ -272,4 +272,28 @@ def test_step_count_matches_oracle(counter_clock):
     _, total = S.render(h, None, None, [1, 0.4, 0.6], [1, 1, 1], [256, 256], np.flip(r.RotationMatrix, 0),
                         [0, 3, 6], 0.9, [1, 1, 0])
     assert abs(int(steps[0].item()) - total) <= total * 1e-4, (int(steps[0].item()), total)
+    r.delete()
+
+
+@pytest.mark.parametrize("scene", ["hg2", "lookup", "ea"])
+def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene):
+    """The LDS-staged march, the plain kernel, the empty-sample skip / empty-chunk leap and the
+    XCD tile order change only where data comes from and which exact no-ops are elided: the
+    images must agree bit for bit."""
+    v = vr.Volume(O.shell_volume(56))
+    r = ex1_renderer(v, res=(120, 88), lights=(scene != "ea"))
+    if scene == "lookup":
+        r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
+    imgs = {}
+    for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
+                      ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"})]:
+        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        imgs[name] = r.render()
+    base = imgs["default"]
+    assert base.max() > 0
+    for name, img in imgs.items():
+        assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
     r.delete()

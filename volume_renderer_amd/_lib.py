@@ -10,7 +10,7 @@ import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvrhip.so")
+LIB_PATH = os.environ.get("VR_LIB_PATH") or os.path.join(_HERE, "libvrhip.so")  # override: A/B builds
 
 VR_OK = 0
 VR_HOST = 0

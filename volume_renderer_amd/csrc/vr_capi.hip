@@ -30,6 +30,7 @@
 
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
+hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
@@ -430,6 +431,18 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
     F.share = em_grid && P.gx.p && P.gy.p && P.gz.p && !P.gx.one && same_dims(P.gx, P.em) &&
               same_dims(P.gy, P.em) && same_dims(P.gz, P.em);
   P.re_is_em = same_tex(P.re, P.em) && P.em.p != nullptr;
+  // staging halo per axis, in emission texels (vr_march.hip axis_range): the gradient tap offset
+  // gstep * bscale * n (0.5 for a cube) plus a margin that bounds the drift between a predicted
+  // position fma(step, k, pos) and k sequentially rounded additions (k <= 64, |pos| <= |box| + |eye|)
+  {
+    double pmax = 0.0;
+    for (int i = 0; i < 3; ++i) pmax = std::max(pmax, (double)std::fabs(P.bmin[i]) + std::fabs(P.eye[i]));
+    for (int i = 0; i < 3; ++i) {
+      const float n = i == 0 ? P.em.fnx : (i == 1 ? P.em.fny : P.em.fnz);
+      const double drift = 64.0 * 2.0 * pmax * 1.2e-7 * (double)P.bscale[i] * (double)n;
+      P.tap_off[i] = (float)((F.mode == 1 ? (double)P.gstep[i] * P.bscale[i] * n : 0.0) + 0.0625 + drift);
+    }
+  }
   // Empty-sample skip: a sample with alpha == 0 adds fma(eds, c, ill) * 0 to the
   // sum; that is exactly +-0 (a no-op) whenever the illumination term `ill` is finite, which holds
   // if the reflection texture, the LUT, the light colours, the colour and Fr are finite and small.
@@ -508,6 +521,11 @@ int validate_partition(const vr_partition *p) {
   return VR_OK;
 }
 
+bool env_flag(const char *name) {
+  const char *ev = std::getenv(name);
+  return ev && ev[0] == '1';
+}
+
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
               unsigned long long *d_steps, hipStream_t stream, Frame &F) {
@@ -535,12 +553,21 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   P.plane_cols = (int32_t)part_columns(P.width, P.block_cols, 0, P.num_parts);
   P.out = d_out;
   P.steps = d_steps;
+  P.tile_mode = 0;
+  if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
   if (F.degenerate) {
     if (out_bytes) VR_HIP(hipMemsetAsync(d_out, 0, out_bytes, stream));
     return VR_OK;
   }
-  VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
+  // LDS-staged march (vr_march.hip) whenever the emission texture is a real grid and, for the
+  // on-the-fly gradient, is also the gradient texture; the plain kernel covers everything else.
+  const bool march = P.em.p && !P.em.one && (F.mode != 1 || F.share) && !env_flag("VR_NO_LDS");
+  if (march) {
+    VR_HIP(vr::launch_march(P, F.mode, F.ab_alias, F.share, stream));
+  } else {
+    VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
+  }
   return VR_OK;
 }
 

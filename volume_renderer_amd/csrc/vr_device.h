@@ -46,11 +46,13 @@ struct RenderParams {
                                   // by a terminating ray, stops the reference's t-stall hang)
   float color[3];
   float gstep[3];                 // gradient step (world units)          volumeRender.cpp:273-275
+  float tap_off[3];               // gradient tap offset in emission texels (staging halo)
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
+  int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles
   // image-space partition (vr_partition): local column lc -> global column
   int32_t block_cols, part, num_parts, part_cols;
   int32_t plane_cols;             // column stride of the output planes (part 0's column count)

@@ -23,94 +23,22 @@
 #include <math.h>
 
 #include "vr_device.h"
+#include "vr_sampling.h"
 
 namespace vr {
-
-#define VR_PI ((float)3.14159265358979323846f)  // volumeRender_kernel.cu:20
-#define VR_INV_PI 0.318309886183790671538f
-
-struct f3 {
-  float x, y, z;
-};
-__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
-__device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-
-typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
-
-// acos(x) / pi for x in [-1, 1] (NaN outside, like acosf): A&S 4.4.46, |err| <= 2e-8 + rounding
-__device__ __forceinline__ float acos_over_pi(float x) {
-  const float a = fabsf(x);
-  float p = -0.0012624911f;
-  p = fmaf(p, a, 0.0066700901f);
-  p = fmaf(p, a, -0.0170881256f);
-  p = fmaf(p, a, 0.0308918810f);
-  p = fmaf(p, a, -0.0501743046f);
-  p = fmaf(p, a, 0.0889789874f);
-  p = fmaf(p, a, -0.2145988016f);
-  p = fmaf(p, a, 1.5707963050f);
-  const float r = __builtin_amdgcn_sqrtf(1.f - a) * p * VR_INV_PI;  // acos(|x|)/pi
-  return x < 0.f ? 1.f - r : r;
-}
-
-// One axis of the linear-filter address computation (normalized coords, clamp addressing):
-// pair base i' = clamp(floor(c*n - 0.5), -1, n-1) and the 8-bit weight.
-struct Ax {
-  int i;
-  float w;
-};
-__device__ __forceinline__ Ax axis(float c, int n, float fn) {
-  c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
-  const float xb = c * fn - 0.5f;
-  const float fl = floorf(xb);
-  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
-  const int i = (int)fl;
-  return Ax{min(max(i, -1), n - 1), w};
-}
-
-__device__ __forceinline__ float lerp(float a, float b, float w) { return fmaf(w, b - a, a); }
-
-// Trilinear fetch from the apron layout given the three axes.
-template <bool BIG>
-__device__ __forceinline__ float fetch(const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
-  const float *b;
-  if (BIG) {
-    const uint64_t o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
-    b = t.p + o;
-  } else {
-    const uint32_t o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
-    b = t.p + o;
-  }
-  const f2a4 r00 = *reinterpret_cast<const f2a4 *>(b);
-  const f2a4 r10 = *reinterpret_cast<const f2a4 *>(b + t.px);
-  const f2a4 r01 = *reinterpret_cast<const f2a4 *>(b + t.pxy);
-  const f2a4 r11 = *reinterpret_cast<const f2a4 *>(b + t.pxy + t.px);
-  const float c00 = lerp(r00.x, r00.y, ax.w), c10 = lerp(r10.x, r10.y, ax.w);
-  const float c01 = lerp(r01.x, r01.y, ax.w), c11 = lerp(r11.x, r11.y, ax.w);
-  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
-  return lerp(c0, c1, az.w);
-}
-
-// tex3D on any texture state (unbound -> 0, 1x1x1 -> single voxel through the same lerp algebra).
-template <bool BIG>
-__device__ __forceinline__ float tex3d(const DevTex &t, float x, float y, float z) {
-  if (t.p == nullptr) return 0.f;  // wave-uniform
-  if (t.one) {
-    const float v = t.p[0];
-    return fmaf(0.5f, v - v, v);  // == lerp(v, v, w) for every w (NaN/inf/-0 included)
-  }
-  return fetch<BIG>(t, axis(x, t.nx, t.fnx), axis(y, t.ny, t.fny), axis(z, t.nz, t.fnz));
-}
 
 // MODE 0: no light sources (shade() contributes exactly 0); 1: on-the-fly gradient; 2: lookup.
 // SHARE: the gradient texture(s) have the emission texture's dims, so the unshifted axes of the
 // gradient taps (MODE 1) / all axes of the lookups (MODE 2) are the centre sample's.
 template <int MODE, bool AB_ALIAS, bool BIG, bool COUNT, bool SHARE>
-__global__ __launch_bounds__(256) void render_kernel(const RenderParams P) {
+__global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderParams P) {
   // 16x16 pixel workgroup tile; wave w owns the 8x8 quadrant (w & 1, w >> 1); lane -> (x, y)
   // with y fastest so that the column-major output stores of a lane octet are contiguous.
+  int tx, ty;
+  if (!tile_of_block(P, tx, ty)) return;  // whole workgroup: uniform
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lc = blockIdx.x * 16 + (wave & 1) * 8 + (lane >> 3);  // local (partition) column
-  const int y = blockIdx.y * 16 + (wave >> 1) * 8 + (lane & 7);
+  const int lc = tx * 16 + (wave & 1) * 8 + (lane >> 3);  // local (partition) column
+  const int y = ty * 16 + (wave >> 1) * 8 + (lane & 7);
   const bool active = (lc < P.part_cols) && (y < P.height);
   int32_t nsteps = 0, nlit = 0;
   if (active) {
@@ -393,7 +321,13 @@ static hipError_t launch2(const RenderParams &P, bool ab_alias, bool big, bool s
 
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s) {
   if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
-  dim3 grid((unsigned)((P.part_cols + 15) / 16), (unsigned)((P.height + 15) / 16));
+  const uint64_t ntx = (P.part_cols + 15) / 16, nty = (P.height + 15) / 16;
+  uint64_t blocks = ntx * nty;
+  if (P.tile_mode == 1) {
+    const uint64_t nsuper = ((ntx + 7) / 8) * ((nty + 7) / 8);
+    blocks = ((nsuper + 7) / 8) * 512;
+  }
+  dim3 grid((unsigned)blocks);
   switch (mode) {
     case 0: return launch2<0>(P, ab_alias, big, false, grid, s);
     case 1: return launch2<1>(P, ab_alias, big, share, grid, s);

@@ -1,0 +1,188 @@
+// vr_sampling.h -- device helpers shared by the gfx950 kernels: vector ops with the oracle's fma
+// contraction, the CUDA linear-filter address computation (normalized coords, clamp) and the
+// trilinear fetch from the apron layout of vr_device.h.  See DESIGN.md s4 for the arithmetic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "vr_device.h"
+
+namespace vr {
+
+#define VR_PI ((float)3.14159265358979323846f)  // volumeRender_kernel.cu:20
+
+struct f3 {
+  float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+
+typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+// One axis of the linear-filter address computation (normalized coords, clamp addressing):
+// pair base i' = clamp(floor(c*n - 0.5), -1, n-1) and the 8-bit weight.
+struct Ax {
+  int i;
+  float w;
+};
+__device__ __forceinline__ Ax axis(float c, int n, float fn) {
+  c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
+  const float xb = c * fn - 0.5f;
+  const float fl = floorf(xb);
+  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
+  const int i = (int)fl;
+  return Ax{min(max(i, -1), n - 1), w};
+}
+
+__device__ __forceinline__ float lerp(float a, float b, float w) { return fmaf(w, b - a, a); }
+
+// Trilinear fetch from the apron layout given the three axes.
+template <bool BIG>
+__device__ __forceinline__ float fetch(const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
+  const float *b;
+  if (BIG) {
+    const uint64_t o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
+    b = t.p + o;
+  } else {
+    const uint32_t o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
+    b = t.p + o;
+  }
+  const f2a4 r00 = *reinterpret_cast<const f2a4 *>(b);
+  const f2a4 r10 = *reinterpret_cast<const f2a4 *>(b + t.px);
+  const f2a4 r01 = *reinterpret_cast<const f2a4 *>(b + t.pxy);
+  const f2a4 r11 = *reinterpret_cast<const f2a4 *>(b + t.pxy + t.px);
+  const float c00 = lerp(r00.x, r00.y, ax.w), c10 = lerp(r10.x, r10.y, ax.w);
+  const float c01 = lerp(r01.x, r01.y, ax.w), c11 = lerp(r11.x, r11.y, ax.w);
+  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
+  return lerp(c0, c1, az.w);
+}
+
+// tex3D on any texture state (unbound -> 0, 1x1x1 -> single voxel through the same lerp algebra).
+template <bool BIG>
+__device__ __forceinline__ float tex3d(const DevTex &t, float x, float y, float z) {
+  if (t.p == nullptr) return 0.f;  // wave-uniform
+  if (t.one) {
+    const float v = t.p[0];
+    return fmaf(0.5f, v - v, v);  // == lerp(v, v, w) for every w (NaN/inf/-0 included)
+  }
+  return fetch<BIG>(t, axis(x, t.nx, t.fnx), axis(y, t.ny, t.fny), axis(z, t.nz, t.fnz));
+}
+
+
+#ifndef VR_MIN_WAVES
+#define VR_MIN_WAVES 1
+#endif
+
+// Workgroup -> 16x16-pixel tile.  tile_mode 1 (XCD-aware): workgroups are dealt
+// round-robin to the 8 XCDs (b % 8 share one, observed -- a speed assumption only), so block b
+// is mapped to tile `within` of super-tile s = (b/8/64)*8 + b%8, a super-tile being 8x8 tiles
+// (128x128 pixels): each XCD's L2 then serves the rays of one or two compact image regions
+// instead of 128 scattered tiles.  The map is a bijection onto the padded super-tile grid;
+// blocks past the image do nothing.
+__device__ __forceinline__ bool tile_of_block(const RenderParams &P, int &tx, int &ty) {
+  const int b = blockIdx.x;
+  const int ntx = (P.part_cols + 15) >> 4, nty = (P.height + 15) >> 4;
+  if (P.tile_mode == 0) {
+    tx = b % ntx;
+    ty = b / ntx;
+  } else {
+    const int nsx = (ntx + 7) >> 3;
+    const int j = b >> 3, s = ((j >> 6) << 3) + (b & 7), w = j & 63;
+    tx = (s % nsx) * 8 + (w & 7);
+    ty = (s / nsx) * 8 + (w >> 3);
+  }
+  return tx < ntx && ty < nty;
+}
+
+// Primary ray of pixel (x, y) and its box intersection (volumeRender_kernel.cu:388-425), op for
+// op as the oracle.  Returns hit; tnear is already clamped to 0.
+__device__ __forceinline__ bool ray_setup(const RenderParams &P, int x, int y, f3 &o, f3 &d, float &tnear,
+                                          float &tfar) {
+  const float u = fmaf((float)x / P.fw, 2.f, -1.f);
+  const float v = fmaf(((float)y / P.fh) * 2.f, P.ratio, -P.ratio);
+  o = mk(P.eye[0], P.eye[1], P.eye[2]);
+  f3 du;
+  du.x = fmaf(P.focal, P.zdir[0], fmaf(v, P.ydir[0], u * P.nx_[0]));
+  du.y = fmaf(P.focal, P.zdir[1], fmaf(v, P.ydir[1], u * P.nx_[1]));
+  du.z = fmaf(P.focal, P.zdir[2], fmaf(v, P.ydir[2], u * P.nx_[2]));
+  const float inv = 1.f / sqrtf(dot3(du, du));
+  d = mk(du.x * inv, du.y * inv, du.z * inv);
+  const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
+  const f3 bmax = mk(-P.bmin[0], -P.bmin[1], -P.bmin[2]);
+  const f3 id = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+  float tmin = ((id.x < 0.f ? bmax.x : bmin.x) - o.x) * id.x;
+  float tmax = ((id.x < 0.f ? bmin.x : bmax.x) - o.x) * id.x;
+  const float tymin = ((id.y < 0.f ? bmax.y : bmin.y) - o.y) * id.y;
+  const float tymax = ((id.y < 0.f ? bmin.y : bmax.y) - o.y) * id.y;
+  bool hit = !((tmin > tymax) || (tymin > tmax));
+  if (tymin > tmin) tmin = tymin;
+  if (tymax < tmax) tmax = tymax;
+  const float tzmin = ((id.z < 0.f ? bmax.z : bmin.z) - o.z) * id.z;
+  const float tzmax = ((id.z < 0.f ? bmin.z : bmax.z) - o.z) * id.z;
+  hit = hit && !((tmin > tzmax) || (tzmin > tmax));
+  if (tzmin > tmin) tmin = tzmin;
+  if (tzmax < tmax) tmax = tzmax;
+  tnear = tmin < 0.f ? 0.f : tmin;
+  tfar = tmax;
+  return hit;
+}
+
+// shade() of volumeRender_kernel.cu:308-353 after the gradient: per light, the three angles and
+// the LUT lookup, accumulated as ((refl*light)*lc)*color + result.  `refl` is Fr * R(p).
+#ifndef VR_ABLATE
+#define VR_ABLATE 0  // diagnostic builds only (tools/ablate.sh): 1 LUT, 2 angles, 4 taps, 8 exp
+#endif
+
+__device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
+                                             const float refl, float &ir, float &ig, float &ib) {
+  // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
+  // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n below
+  // cancel when the view ray is parallel to n, and gamma then depends on every bit of n.
+  const float ginv = 1.f / sqrtf(dot3(g, g));
+  const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
+  const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
+  // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle
+  const float nlen = sqrtf(dot3(n, n));
+#if VR_ABLATE & 2
+  const float alpha_n = dot3(n, li) * 0.1f;
+#else
+  const float alpha_n = acosf(dot3(n, li) / (nlen * sqrtf(dot3(li, li)))) / VR_PI;
+#endif
+  const float dli = dot3(li, n);
+  const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
+  const float liplen = sqrtf(dot3(lip, lip));
+  const Ax la = axis(alpha_n, P.lut.nx, P.lut.fnx);
+  for (int i = 0; i < P.num_lights; ++i) {
+    const DevLight L = P.lights[i];
+    const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);  // lightOut
+#if VR_ABLATE & 2
+    const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
+#else
+    const float beta = acosf(dot3(n, lo) / (nlen * sqrtf(dot3(lo, lo)))) / VR_PI;
+    const float dlo = dot3(lo, n);
+    const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
+    const float gamma = acosf(dot3(lip, lop) / (liplen * sqrtf(dot3(lop, lop)))) / VR_PI;
+#endif
+    float light = 0.f;
+#if VR_ABLATE & 1
+    light = beta + gamma + la.w;
+    if (false) {
+#else
+    if (P.lut.p != nullptr) {
+#endif
+      if (P.lut.one) {
+        const float q = P.lut.p[0];
+        light = fmaf(0.5f, q - q, q);
+      } else {
+        light = fetch<false>(P.lut, la, axis(beta, P.lut.ny, P.lut.fny), axis(gamma, P.lut.nz, P.lut.fnz));
+      }
+    }
+    const float rl = refl * light;
+    ir = fmaf(rl * L.cr, P.color[0], ir);
+    ig = fmaf(rl * L.cg, P.color[1], ig);
+    ib = fmaf(rl * L.cb, P.color[2], ib);
+  }
+}
+
+}  // namespace vr
