@@ -30,7 +30,7 @@
 
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
-hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, hipStream_t s);
+hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
@@ -562,9 +562,10 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   }
   // LDS-staged march (vr_march.hip) whenever the emission texture is a real grid and, for the
   // on-the-fly gradient, is also the gradient texture; the plain kernel covers everything else.
+  // Both produce bit-identical images (tests/test_gpu_parity.py::test_kernel_variants...).
   const bool march = P.em.p && !P.em.one && (F.mode != 1 || F.share) && !env_flag("VR_NO_LDS");
   if (march) {
-    VR_HIP(vr::launch_march(P, F.mode, F.ab_alias, F.share, stream));
+    VR_HIP(vr::launch_march(P, F.mode, F.ab_alias, F.share, F.big, stream));
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
   }

@@ -18,110 +18,13 @@
 
 #include "vr_device.h"
 #include "vr_sampling.h"
+#include "vr_stage.h"
 
 namespace vr {
 
-#ifndef VR_LDS_CAP
-#define VR_LDS_CAP 2048  // floats per wave slot (8 KiB; 4 slots = 32 KiB per workgroup)
-#endif
-#ifndef VR_CHUNK
-#define VR_CHUNK 32      // samples per staged chunk (halved while the box does not fit)
-#endif
-
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return __builtin_amdgcn_readfirstlane(v);
-}
-
-// Staged box: padded-volume index ranges [r0, r0 + e) per axis.
-struct Box {
-  int rx, ry, rz, ex, ey, ez;
-};
-
-// Global fetch with 64-bit addressing (the fallback path; any volume size).
-__device__ __forceinline__ float fetch_global(const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
-  return fetch<true>(t, ax, ay, az);
-}
-
-// Trilinear fetch of the staged emission texture: LDS when the 2x2x2 cell lies in the box.
-__device__ __forceinline__ float fetch_em(const DevTex &t, const float *L, const Box &B, bool staged,
-                                          const Ax &ax, const Ax &ay, const Ax &az) {
-  if (staged) {
-    const int lx = ax.i + 1 - B.rx, ly = ay.i + 1 - B.ry, lz = az.i + 1 - B.rz;
-    if ((unsigned)lx < (unsigned)(B.ex - 1) && (unsigned)ly < (unsigned)(B.ey - 1) &&
-        (unsigned)lz < (unsigned)(B.ez - 1)) {
-      const int a = (lz * B.ey + ly) * B.ex + lx;
-      const int exy = B.ex * B.ey;
-      const float c00 = lerp(L[a], L[a + 1], ax.w);
-      const float c10 = lerp(L[a + B.ex], L[a + B.ex + 1], ax.w);
-      const float c01 = lerp(L[a + exy], L[a + exy + 1], ax.w);
-      const float c11 = lerp(L[a + exy + B.ex], L[a + exy + B.ex + 1], ax.w);
-      const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
-      return lerp(c0, c1, az.w);
-    }
-  }
-  return fetch_global(t, ax, ay, az);
-}
-
-// Padded index range [lo, hi] (inclusive) of the tap pairs of one axis for a coordinate range.
-// `off` includes the staging margin (RenderParams::tap_off): it bounds the drift between the
-// predicted end position fma(step, k, pos) and the k sequentially rounded pos += step additions.
-__device__ __forceinline__ void axis_range(float c0, float c1, float off, int n, int &lo, int &hi) {
-  const float cmin = fminf(c0, c1) - off, cmax = fmaxf(c0, c1) + off;
-  const int a = (int)floorf(cmin), b = (int)floorf(cmax);
-  lo = min(max(a, -1), n - 1) + 1;
-  hi = min(max(b, -1), n - 1) + 2;
-}
-
-// Copy box B of the apron volume into the wave's LDS slot (row-major, x fastest).  Returns
-// whether any staged voxel is non-zero (NaN counts as non-zero), for the whole wave.
-__device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &B, int lane) {
-  bool nz = false;
-  const uint32_t ex = (uint32_t)B.ex, ey = (uint32_t)B.ey;
-  const uint32_t V = ex * ey * (uint32_t)B.ez;
-  uint32_t x = (uint32_t)lane % ex;
-  uint32_t r = (uint32_t)lane / ex;
-  uint32_t y = r % ey, z = r / ey;
-  const uint32_t sx = 64u % ex, sr = 64u / ex;
-  for (uint32_t q0 = (uint32_t)lane; q0 < V; q0 += 256u) {
-    float v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t q = q0 + 64u * j;
-      if (q < V) {
-        const uint64_t o = ((uint64_t)(B.rz + z) * t.pxy + (uint64_t)(B.ry + y) * t.px) + (uint64_t)(B.rx + x);
-        v[j] = t.p[o];
-        nz |= (v[j] != 0.f);
-      }
-      x += sx;
-      y += sr;
-      if (x >= ex) {
-        x -= ex;
-        ++y;
-      }
-      while (y >= ey) {
-        y -= ey;
-        ++z;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t q = q0 + 64u * j;
-      if (q < V) L[q] = v[j];
-    }
-  }
-  return __any(nz);
-}
-
 // MODE 0: no lights; 1: on-the-fly gradient from the staged emission texture (gem == em);
 // 2: lookup gradient (gx/gy/gz from global memory at the centre's axes when dims match).
-template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2>
+template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG>
 __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
   __shared__ float lds[4][VR_LDS_CAP];
   int tx, ty;
@@ -134,6 +37,7 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
   const DevTex &E = P.em;
   int32_t nsteps = 0, nlit = 0;
   uint32_t c_staged = 0, c_leap = 0, c_fall = 0;  // chunk statistics (COUNT builds)
+  uint32_t w_iter = 0, w_lit = 0;                  // wave sample iterations, of which with shading
   float sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f;
   f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f), pos = o, step = o;
   float t = 0.f, tfar = -1.f;
@@ -153,54 +57,20 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
 
   while (__any(alive)) {
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
-    int S = VR_CHUNK;
-    bool staged = false;
-    Box B{0, 0, 0, 1, 1, 1};
-    for (int attempt = 0; attempt < 3; ++attempt, S >>= 1) {
-      int lo[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, hi[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
-      if (alive) {
-        const float rem = (tfar - t) / tstep;  // samples left before the exit test fires
-        const int s_eff = (rem < (float)S) ? max((int)rem + 2, 1) : S;
-        const float k = (float)(s_eff - 1);
-        const f3 pe = mk(fmaf(step.x, k, pos.x), fmaf(step.y, k, pos.y), fmaf(step.z, k, pos.z));
-        axis_range(((pos.x - bmin.x) * bsc.x) * E.fnx - 0.5f, ((pe.x - bmin.x) * bsc.x) * E.fnx - 0.5f,
-                   P.tap_off[0], E.nx, lo[0], hi[0]);
-        axis_range(((pos.y - bmin.y) * bsc.y) * E.fny - 0.5f, ((pe.y - bmin.y) * bsc.y) * E.fny - 0.5f,
-                   P.tap_off[1], E.ny, lo[1], hi[1]);
-        axis_range(((pos.z - bmin.z) * bsc.z) * E.fnz - 0.5f, ((pe.z - bmin.z) * bsc.z) * E.fnz - 0.5f,
-                   P.tap_off[2], E.nz, lo[2], hi[2]);
-      }
-      B.rx = wave_min(lo[0]);
-      B.ry = wave_min(lo[1]);
-      B.rz = wave_min(lo[2]);
-      B.ex = wave_max(hi[0]) - B.rx + 1;
-      B.ey = wave_max(hi[1]) - B.ry + 1;
-      B.ez = wave_max(hi[2]) - B.rz + 1;
-      if (B.ex > 0 && B.ey > 0 && B.ez > 0 && B.ex * B.ey * B.ez <= VR_LDS_CAP) {
-        staged = true;
-        break;
-      }
-      if (attempt == 2) S = 8;  // no box fits: march 8 samples from global memory
-    }
+    int S;
+    bool staged;
+    Box B;
+    plan_chunk(P, alive, pos, step, t, tfar, S, staged, B);
     bool empty = false;
-    if (staged) empty = P.skip_empty && !stage_box(L, E, B, lane);
+    if (staged) {
+      const bool nonzero = stage_box(L, E, B, lane);  // always stage: the samples read the slot
+      empty = P.skip_empty && !nonzero;
+    }
     __builtin_amdgcn_wave_barrier();
     if (COUNT) ++(staged ? (empty ? c_leap : c_staged) : c_fall);
 
     if (empty) {
-      // Every tap of every sample of this chunk lies in the staged box and the box is all zero:
-      // each sample has em = ab = 0, alpha = 1 - exp(-0) = 0 and adds exactly 0 (skip_empty
-      // proves the shading term finite).  Only the march recurrences run, in the same order.
-      for (int k = 0; k < S && alive; ++k) {
-        ++nsteps;
-        if (nsteps >= P.max_steps) {
-          alive = false;
-        } else {
-          t += tstep;
-          if (t > tfar) alive = false;
-          else pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
-        }
-      }
+      leap(P, S, alive, nsteps, t, tfar, pos, step);
       continue;
     }
 
@@ -208,8 +78,8 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
     for (int k = 0; k < S && alive; ++k) {
       const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
       const Ax ax = axis(ps.x, E.nx, E.fnx), ay = axis(ps.y, E.ny, E.fny), az = axis(ps.z, E.nz, E.fnz);
-      const float em_s = fetch_em(E, L, B, staged, ax, ay, az);
-      const float ab_s = AB_ALIAS ? em_s : tex3d<true>(P.ab, ps.x, ps.y, ps.z);
+      const float em_s = fetch_em<BIG>(E, L, B, staged, ax, ay, az);
+      const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
       const float e = P.fe * em_s;
       const float a = P.fa * ab_s;
 #if VR_ABLATE & 8
@@ -220,6 +90,10 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
       const float eds = e * tstep;
       float ir = 0.f, ig = 0.f, ib = 0.f;
       const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
+      if (COUNT) {
+        ++w_iter;
+        w_lit += (MODE != 0 && __any(!skip)) ? 1u : 0u;
+      }
       if (MODE != 0 && !skip) {
         if (COUNT) ++nlit;
         f3 g;
@@ -232,20 +106,20 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
           const float ym = ((pos.y - P.gstep[1]) - bmin.y) * bsc.y;
           const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
           const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
-          g.x = fetch_em(E, L, B, staged, axis(xp, E.nx, E.fnx), ay, az) -
-                fetch_em(E, L, B, staged, axis(xm, E.nx, E.fnx), ay, az);
-          g.y = fetch_em(E, L, B, staged, ax, axis(yp, E.ny, E.fny), az) -
-                fetch_em(E, L, B, staged, ax, axis(ym, E.ny, E.fny), az);
-          g.z = fetch_em(E, L, B, staged, ax, ay, axis(zp, E.nz, E.fnz)) -
-                fetch_em(E, L, B, staged, ax, ay, axis(zm, E.nz, E.fnz));
+          g.x = fetch_em<BIG>(E, L, B, staged, axis(xp, E.nx, E.fnx), ay, az) -
+                fetch_em<BIG>(E, L, B, staged, axis(xm, E.nx, E.fnx), ay, az);
+          g.y = fetch_em<BIG>(E, L, B, staged, ax, axis(yp, E.ny, E.fny), az) -
+                fetch_em<BIG>(E, L, B, staged, ax, axis(ym, E.ny, E.fny), az);
+          g.z = fetch_em<BIG>(E, L, B, staged, ax, ay, axis(zp, E.nz, E.fnz)) -
+                fetch_em<BIG>(E, L, B, staged, ax, ay, axis(zm, E.nz, E.fnz));
           g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
         } else if (SHARE2) {
-          g = mk(fetch_global(P.gx, ax, ay, az), fetch_global(P.gy, ax, ay, az), fetch_global(P.gz, ax, ay, az));
+          g = mk(fetch<BIG>(P.gx, ax, ay, az), fetch<BIG>(P.gy, ax, ay, az), fetch<BIG>(P.gz, ax, ay, az));
         } else {
-          g = mk(tex3d<true>(P.gx, ps.x, ps.y, ps.z), tex3d<true>(P.gy, ps.x, ps.y, ps.z),
-                 tex3d<true>(P.gz, ps.x, ps.y, ps.z));
+          g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
+                 tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
         }
-        const float refl = P.fr * (P.re_is_em ? em_s : tex3d<true>(P.re, ps.x, ps.y, ps.z));
+        const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
         shade_lights(P, g, pos, o, refl, ir, ig, ib);
       }
       const float r = fmaf(eds, P.color[0], ir) * alpha;
@@ -287,22 +161,27 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
       atomicAdd(P.steps + 2, (unsigned long long)c_staged);
       atomicAdd(P.steps + 3, (unsigned long long)c_leap);
       atomicAdd(P.steps + 4, (unsigned long long)c_fall);
+      atomicAdd(P.steps + 5, (unsigned long long)w_iter);
+      atomicAdd(P.steps + 6, (unsigned long long)w_lit);
     }
   }
 }
 
 template <int MODE, bool AB, bool SH>
-static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s) {
-  if (P.steps)
-    hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH>), grid, dim3(256), 0, s, P);
-  else
-    hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH>), grid, dim3(256), 0, s, P);
+static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
+  if (P.steps) {
+    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, true>), grid, dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, false>), grid, dim3(256), 0, s, P);
+  } else {
+    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, true>), grid, dim3(256), 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, false>), grid, dim3(256), 0, s, P);
+  }
   return hipGetLastError();
 }
 
 // Host entry: the staged kernel needs a bound, non-constant emission texture; for MODE 1 the
 // gradient texture must be the emission texture itself (the reference's tex_emission binding).
-hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, hipStream_t s) {
+hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s) {
   if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
   const uint64_t ntx = (P.part_cols + 15) / 16, nty = (P.height + 15) / 16;
   uint64_t blocks = ntx * nty;
@@ -312,11 +191,11 @@ hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool sha
   }
   const dim3 grid((unsigned)blocks);
   switch (mode) {
-    case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s) : launch_m<0, false, false>(P, grid, s);
-    case 1: return ab_alias ? launch_m<1, true, false>(P, grid, s) : launch_m<1, false, false>(P, grid, s);
+    case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);
+    case 1: return ab_alias ? launch_m<1, true, false>(P, grid, s, big) : launch_m<1, false, false>(P, grid, s, big);
     default:
-      if (share) return ab_alias ? launch_m<2, true, true>(P, grid, s) : launch_m<2, false, true>(P, grid, s);
-      return ab_alias ? launch_m<2, true, false>(P, grid, s) : launch_m<2, false, false>(P, grid, s);
+      if (share) return ab_alias ? launch_m<2, true, true>(P, grid, s, big) : launch_m<2, false, true>(P, grid, s, big);
+      return ab_alias ? launch_m<2, true, false>(P, grid, s, big) : launch_m<2, false, false>(P, grid, s, big);
   }
 }
 

@@ -131,8 +131,18 @@ __device__ __forceinline__ bool ray_setup(const RenderParams &P, int x, int y, f
 // shade() of volumeRender_kernel.cu:308-353 after the gradient: per light, the three angles and
 // the LUT lookup, accumulated as ((refl*light)*lc)*color + result.  `refl` is Fr * R(p).
 #ifndef VR_ABLATE
-#define VR_ABLATE 0  // diagnostic builds only (tools/ablate.sh): 1 LUT, 2 angles, 4 taps, 8 exp
+#define VR_ABLATE 0  // diagnostic builds only (tools/ablate_build.sh): 1 LUT, 2 angles, 4 taps, 8 exp,
+                     // 16 no staged-box check
 #endif
+
+// x / pi, correctly rounded, for x = 0, NaN or x >= 2^-100 -- the range of acosf: x * RN(1/pi)
+// corrected by one fma residual step (3 VALU instead of the 12 of a general IEEE divide).  Equal to
+// the IEEE quotient for every such fp32 x (exhaustive check: tools/microbench/divpi_check.c).
+__device__ __forceinline__ float divpi(float x) {
+  const float r = 0x1.45f306p-2f;  // RN(1 / (float)pi)
+  const float q = x * r;
+  return fmaf(fmaf(-q, VR_PI, x), r, q);
+}
 
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib) {
@@ -147,7 +157,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #if VR_ABLATE & 2
   const float alpha_n = dot3(n, li) * 0.1f;
 #else
-  const float alpha_n = acosf(dot3(n, li) / (nlen * sqrtf(dot3(li, li)))) / VR_PI;
+  const float alpha_n = divpi(acosf(dot3(n, li) / (nlen * sqrtf(dot3(li, li)))));
 #endif
   const float dli = dot3(li, n);
   const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
@@ -159,10 +169,10 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #if VR_ABLATE & 2
     const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
 #else
-    const float beta = acosf(dot3(n, lo) / (nlen * sqrtf(dot3(lo, lo)))) / VR_PI;
+    const float beta = divpi(acosf(dot3(n, lo) / (nlen * sqrtf(dot3(lo, lo)))));
     const float dlo = dot3(lo, n);
     const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-    const float gamma = acosf(dot3(lip, lop) / (liplen * sqrtf(dot3(lop, lop)))) / VR_PI;
+    const float gamma = divpi(acosf(dot3(lip, lop) / (liplen * sqrtf(dot3(lop, lop)))));
 #endif
     float light = 0.f;
 #if VR_ABLATE & 1

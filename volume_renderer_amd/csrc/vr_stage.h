@@ -1,0 +1,179 @@
+// vr_stage.h -- per-wave LDS staging of the emission volume for the march kernels:
+// wave reductions, the staged box, the tap-pair range of a chunk, the box copy and the trilinear
+// fetch that reads the slot when the 2x2x2 cell lies in it (global memory otherwise, same
+// arithmetic).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "vr_device.h"
+#include "vr_sampling.h"
+
+namespace vr {
+
+#ifndef VR_LDS_CAP
+#define VR_LDS_CAP 2560  // floats per wave slot (10 KiB; 40 KiB per workgroup -> 4 workgroups per CU)
+#endif
+#ifndef VR_CHUNK
+#define VR_CHUNK 32      // samples per staged chunk (halved while the box does not fit)
+#endif
+#ifndef VR_ATTEMPTS
+#define VR_ATTEMPTS 3    // box attempts per chunk: S = VR_CHUNK, /2, /4, ...
+#endif
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+#ifndef VR_ODD_PITCH
+#define VR_ODD_PITCH 0   // 1: odd LDS row / plane pitches (measured slower: larger slots overflow more)
+#endif
+
+// Staged box: padded-volume index ranges [r0, r0 + e) per axis, stored in the slot with row
+// pitch px and plane pitch pxy (odd, so that rows and planes start on rotating banks).
+struct Box {
+  int rx, ry, rz, ex, ey, ez, px, pxy;
+};
+
+// Trilinear fetch of the staged emission texture: LDS when the 2x2x2 cell lies in the box.
+template <bool BIG>
+__device__ __forceinline__ float fetch_em(const DevTex &t, const float *L, const Box &B, bool staged,
+                                          const Ax &ax, const Ax &ay, const Ax &az) {
+  if (staged) {
+    const int lx = ax.i + 1 - B.rx, ly = ay.i + 1 - B.ry, lz = az.i + 1 - B.rz;
+    if ((VR_ABLATE & 16) || ((unsigned)lx < (unsigned)(B.ex - 1) && (unsigned)ly < (unsigned)(B.ey - 1) &&
+                             (unsigned)lz < (unsigned)(B.ez - 1))) {
+      const int a = lz * B.pxy + ly * B.px + lx;
+      const float c00 = lerp(L[a], L[a + 1], ax.w);
+      const float c10 = lerp(L[a + B.px], L[a + B.px + 1], ax.w);
+      const float c01 = lerp(L[a + B.pxy], L[a + B.pxy + 1], ax.w);
+      const float c11 = lerp(L[a + B.pxy + B.px], L[a + B.pxy + B.px + 1], ax.w);
+      const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
+      return lerp(c0, c1, az.w);
+    }
+  }
+  return fetch<BIG>(t, ax, ay, az);
+}
+
+// Padded index range [lo, hi] (inclusive) of the tap pairs of one axis for a coordinate range.
+// `off` includes the staging margin (RenderParams::tap_off): it bounds the drift between the
+// predicted end position fma(step, k, pos) and the k sequentially rounded pos += step additions.
+__device__ __forceinline__ void axis_range(float c0, float c1, float off, int n, int &lo, int &hi) {
+  const float cmin = fminf(c0, c1) - off, cmax = fmaxf(c0, c1) + off;
+  const int a = (int)floorf(cmin), b = (int)floorf(cmax);
+  lo = min(max(a, -1), n - 1) + 1;
+  hi = min(max(b, -1), n - 1) + 2;
+}
+
+// Copy box B of the apron volume into the wave's LDS slot (row-major, x fastest).  Returns
+// whether any staged voxel is non-zero (NaN counts as non-zero), for the whole wave.
+__device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &B, int lane) {
+  bool nz = false;
+  const uint32_t ex = (uint32_t)B.ex, ey = (uint32_t)B.ey;
+  const uint32_t V = ex * ey * (uint32_t)B.ez;
+  uint32_t x = (uint32_t)lane % ex;
+  uint32_t r = (uint32_t)lane / ex;
+  uint32_t y = r % ey, z = r / ey;
+  const uint32_t sx = 64u % ex, sr = 64u / ex;
+  for (uint32_t q0 = (uint32_t)lane; q0 < V; q0 += 256u) {
+    float v[4];
+    uint32_t li[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t q = q0 + 64u * j;
+      li[j] = z * (uint32_t)B.pxy + y * (uint32_t)B.px + x;
+      if (q < V) {
+        const uint64_t o = ((uint64_t)(B.rz + z) * t.pxy + (uint64_t)(B.ry + y) * t.px) + (uint64_t)(B.rx + x);
+        v[j] = t.p[o];
+        nz |= (v[j] != 0.f);
+      }
+      x += sx;
+      y += sr;
+      if (x >= ex) {
+        x -= ex;
+        ++y;
+      }
+      while (y >= ey) {
+        y -= ey;
+        ++z;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t q = q0 + 64u * j;
+      if (q < V) L[li[j]] = v[j];
+    }
+  }
+  return __any(nz);
+}
+
+
+// Chunk set-up: the box of every tap the wave's live rays take in their next S samples, S halved
+// (up to VR_ATTEMPTS tries) until the box fits the slot; staged == false: march 8 samples from
+// global memory.  The predicted end position fma(step, k, pos) is bounded against the k
+// sequentially rounded additions by RenderParams::tap_off.
+__device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, const f3 &pos, const f3 &step,
+                                           float t, float tfar, int &S, bool &staged, Box &B) {
+  const DevTex &E = P.em;
+  const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
+  const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
+  const float tstep = P.tstep;
+  S = VR_CHUNK;
+  staged = false;
+  B = Box{0, 0, 0, 1, 1, 1, 1, 1};
+  for (int attempt = 0; attempt < VR_ATTEMPTS; ++attempt, S >>= 1) {
+    int lo[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, hi[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
+    if (alive) {
+      const float rem = (tfar - t) / tstep;  // samples left before the exit test fires
+      const int s_eff = (rem < (float)S) ? max((int)rem + 2, 1) : S;
+      const float k = (float)(s_eff - 1);
+      const f3 pe = mk(fmaf(step.x, k, pos.x), fmaf(step.y, k, pos.y), fmaf(step.z, k, pos.z));
+      axis_range(((pos.x - bmin.x) * bsc.x) * E.fnx - 0.5f, ((pe.x - bmin.x) * bsc.x) * E.fnx - 0.5f,
+                 P.tap_off[0], E.nx, lo[0], hi[0]);
+      axis_range(((pos.y - bmin.y) * bsc.y) * E.fny - 0.5f, ((pe.y - bmin.y) * bsc.y) * E.fny - 0.5f,
+                 P.tap_off[1], E.ny, lo[1], hi[1]);
+      axis_range(((pos.z - bmin.z) * bsc.z) * E.fnz - 0.5f, ((pe.z - bmin.z) * bsc.z) * E.fnz - 0.5f,
+                 P.tap_off[2], E.nz, lo[2], hi[2]);
+    }
+    B.rx = wave_min(lo[0]);
+    B.ry = wave_min(lo[1]);
+    B.rz = wave_min(lo[2]);
+    B.ex = wave_max(hi[0]) - B.rx + 1;
+    B.ey = wave_max(hi[1]) - B.ry + 1;
+    B.ez = wave_max(hi[2]) - B.rz + 1;
+    B.px = VR_ODD_PITCH ? (B.ex | 1) : B.ex;
+    B.pxy = VR_ODD_PITCH ? ((B.px * B.ey) | 1) : B.px * B.ey;
+    if (B.ex > 0 && B.ey > 0 && B.ez > 0 && B.pxy * B.ez <= VR_LDS_CAP) {
+      staged = true;
+      return;
+    }
+    if (attempt == VR_ATTEMPTS - 1) S = 8;  // no box fits: march 8 samples from global memory
+  }
+}
+
+// The empty-chunk leap: every tap of the chunk lies in the staged all-zero box, so each sample has
+// em = ab = 0, alpha = 1 - exp(-0) = 0 and adds exactly 0 (skip_empty proves the shading term
+// finite).  Only the march recurrences run, in the reference's order.
+__device__ __forceinline__ void leap(const RenderParams &P, int S, bool &alive, int32_t &nsteps, float &t,
+                                     float tfar, f3 &pos, const f3 &step) {
+  for (int k = 0; k < S && alive; ++k) {
+    ++nsteps;
+    if (nsteps >= P.max_steps) {
+      alive = false;
+    } else {
+      t += P.tstep;
+      if (t > tfar) alive = false;
+      else pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
+    }
+  }
+}
+
+}  // namespace vr
