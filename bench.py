@@ -50,9 +50,11 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--block-cols", type=int, default=16, help="column block of the image partition")
-    ap.add_argument("--cpu-stride", type=int, default=16, help="CPU baseline: every k-th column")
+    ap.add_argument("--cpu-stride", type=int, default=8, help="CPU baseline: every k-th column")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round1", "traffic.json"),
+                    help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,6 +222,18 @@ def main():
             "bit_exact_frac": float((g[:, cols, :].view(np.uint32) == o[:, cols, :].view(np.uint32)).mean())}
 
     if rank == 0:
+        # roofline.traffic: HBM bytes per launch from the rocprofv3 PMC passes committed under
+        # profiles/ (FETCH_SIZE + WRITE_SIZE with the gfx950 x2 FETCH_SIZE correction, calibrated
+        # on the stats kernel's known 4.3 GB read); only when it was measured on this workload.
+        try:
+            with open(args.traffic_json) as fh:
+                tj = json.load(fh)
+            if world == 1 and tj.get("workload") == result["config"]["workload"]:
+                result["roofline"]["traffic"] = tj["bytes_per_launch"]
+                result["roofline"]["traffic_source"] = os.path.relpath(args.traffic_json, ROOT) + \
+                    " (" + tj.get("method", "") + ")"
+        except (OSError, ValueError, KeyError):
+            pass
         print(json.dumps(result), flush=True)
     vr.volumeRender("delete", h)
     if world > 1:

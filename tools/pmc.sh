@@ -13,5 +13,5 @@ IFS=';' read -ra GRPS <<< "$PMCG"
 for g in "${GRPS[@]}"; do
   i=$((i+1))
   grp=${g//,/ }
-  timeout -k 10 240 rocprofv3 --pmc $grp -d "$OUT/pass$i" -o pmc --output-format csv -- python bench.py $ARGS > "$OUT/pass$i.log" 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $grp -d "$OUT/pass$i" -o pmc --output-format csv -- python bench.py $ARGS > "$OUT/pass$i.log" 2>&1 || exit 1
 done

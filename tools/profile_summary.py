@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise one measurement pass (tools/r*.sh output under gpurun_out/<run>) into profiles/<round>/:
+kernel_stats.csv (rocprofv3 --kernel-trace --stats), pmc_summary.txt (per-kernel counter averages),
+traffic.json (HBM bytes per launch of the march kernel, read by bench.py for roofline.traffic).
+
+HBM bytes: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128 B request
+(MI355X_MICROARCH.md, HBM section), so read bytes = 2 x 1024 x FETCH_SIZE.  The factor is checked
+here on stats_kernel, which reads every padded voxel once (known byte count).
+usage: tools/profile_summary.py gpurun_out/r13 profiles/round1 WORKLOAD_STRING"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+run, out, workload = sys.argv[1], sys.argv[2], sys.argv[3]
+os.makedirs(out, exist_ok=True)
+ks = glob.glob(os.path.join(run, "kt", "*kernel_stats.csv"))
+if ks:
+    shutil.copy(ks[0], os.path.join(out, "kernel_stats.csv"))
+
+vals = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
+for f in glob.glob(os.path.join(run, "pmc", "pass*", "**", "*counter_collection.csv"), recursive=True):
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            vals[row["Kernel_Name"]][row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+
+lines = []
+for k in sorted(vals):
+    lines.append(k)
+    for c in sorted(vals[k]):
+        per = vals[k][c]
+        lines.append(f"  {c:28s} {sum(per.values()) / len(per):.6g}   (mean over {len(per)} dispatches)")
+with open(os.path.join(out, "pmc_summary.txt"), "w") as fh:
+    fh.write("\n".join(lines) + "\n")
+
+
+def mean(kfilter, counter, exclude="<1, true, true"):
+    xs = [v for k, cs in vals.items() if kfilter in k and exclude not in k for v in cs.get(counter, {}).values()]
+    return sum(xs) / len(xs) if xs else None
+
+
+march = "march_kernel<1, true, false"  # metric config: MODE 1, absorption aliases emission, no counters
+fetch_kb, write_kb = mean(march, "FETCH_SIZE"), mean(march, "WRITE_SIZE")
+if fetch_kb is not None:
+    traffic = 2 * 1024 * fetch_kb + 1024 * (write_kb or 0.0)
+    with open(os.path.join(out, "traffic.json"), "w") as fh:
+        json.dump({"workload": workload, "kernel": march, "fetch_size_kib": fetch_kb, "write_size_kib": write_kb,
+                   "bytes_per_launch": traffic,
+                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; read bytes = 2 x 1024 x FETCH_SIZE "
+                             "(gfx950 64 B tally per 128 B request)"}, fh, indent=1)
+    print("traffic bytes/launch", traffic)
+print("\n".join(lines[:80]))
