@@ -1,0 +1,98 @@
+"""Multi-process partition protocol on CPU: world_size 2 over gloo.
+
+Each rank renders its interleaved column blocks (here with the CPU oracle standing in for the
+GPU kernel: the test is about the partition, the padded part layout and the gather, which are
+backend-agnostic), packs them into the part buffer layout of vr_render_device
+(c*max_cols*H + j*H + y), rank 0 gathers the parts with volume_renderer_amd.parallel and scatters
+them into the full image; the result must equal the single-process render bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from volume_renderer_amd import parallel
+
+W, H, BLOCK = 37, 29, 4
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _scene():
+    vol = O.OVolume(O.shell_volume(24), 10)
+    lut = O.OVolume(O.hg_lut(16, 0.8), 7)
+    lights = np.array([[500, 1000, 550, 0, 1, 1], [0, 550, 90, 1, 0.5, 1]], np.float32)
+    R = O.rotation(125, 25, 0)
+    return vol, lut, lights, R
+
+
+def _render(cols=None):
+    vol, lut, lights, R = _scene()
+    S = O.OracleSession()
+    h = S.new()
+    S.sync_volumes(h, 0, vol, O.OVolume(np.ones((1, 1, 1), np.float32), 5), vol)
+    img, _ = S.render(h, lights, lut, [1.0, 0.4, 0.6], [1, 1, 1], [H, W], np.flip(R, 0).astype(np.float32),
+                      [0, 3.0, 6.0], 0.9, [1, 1, 0], threads=1, cols=cols)
+    S.delete(h)
+    return img  # [H, W, 3]
+
+
+def _assemble(parts: np.ndarray, world: int, max_cols: int) -> np.ndarray:
+    """Host restatement of vr_assemble_partitions: part p's local column j -> global x."""
+    full = np.zeros((H, W, 3), np.float32)
+    for p in range(world):
+        idx = parallel.partition_column_indices(W, BLOCK, p, world)
+        slab = parts[p].reshape(3, max_cols, H)
+        for j, x in enumerate(idx):
+            full[:, x, :] = slab[:, j, :].T
+    return full
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        counts, max_cols = parallel.partition_layout(W, BLOCK, world)
+        idx = parallel.partition_column_indices(W, BLOCK, rank, world)
+        img = _render(cols=idx)
+        buf = np.zeros((3, max_cols, H), np.float32)
+        buf[:, : len(idx), :] = np.transpose(img[:, idx, :], (2, 1, 0))
+        local = torch.from_numpy(buf.reshape(-1))
+        gathered = torch.zeros(world * local.numel()) if rank == 0 else None
+        parallel.gather_partitions(local, gathered, world, rank)
+        if rank == 0:
+            q.put(_assemble(gathered.numpy().reshape(world, -1), world, max_cols))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_partitioned_render_gathers_to_the_full_image(world):
+    ref = _render()
+    assert ref.max() > 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_partition_layout_covers_every_column_once():
+    for world in (1, 2, 3, 8):
+        counts, max_cols = parallel.partition_layout(W, BLOCK, world)
+        allc = np.sort(np.concatenate([parallel.partition_column_indices(W, BLOCK, p, world) for p in range(world)]))
+        assert np.array_equal(allc, np.arange(W)) and sum(counts) == W and max_cols == counts[0]
