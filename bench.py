@@ -102,7 +102,7 @@ def main():
     full = torch.zeros(3 * W * H, dtype=torch.float32, device=dev) if rank == 0 else None
     gathered = (torch.zeros(world * 3 * max_cols * H, dtype=torch.float32, device=dev)
                 if (world > 1 and rank == 0) else None)
-    steps_t = torch.zeros(8, dtype=torch.int64, device=dev)
+    steps_t = torch.zeros(48, dtype=torch.int64, device=dev)
 
     # sample count of this rank's launch (exact, counter variant; untimed)
     mex.render_device(h, ra, out_local.data_ptr(), part, steps_t.data_ptr(), sptr)
@@ -111,6 +111,8 @@ def main():
     my_lit = int(steps_t[1].item())
     chunk_stats = [int(v) for v in steps_t[2:5].tolist()]
     wave_stats = [int(v) for v in steps_t[5:7].tolist()]
+    fail_hist = [int(v) for v in steps_t[8:40].tolist()]
+    staged_by_s = [int(v) for v in steps_t[40:44].tolist()]
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
@@ -183,6 +185,8 @@ def main():
             "shaded_samples_per_frame": total_lit,
             "chunks_staged_leaped_global": chunk_stats,
             "wave_iterations_total_lit": wave_stats,
+            "global_chunk_box_hist_256": fail_hist,
+            "staged_chunks_by_S_32_16_8_4": staged_by_s,
             "gb_per_s_sample_stream": round(4.0 * total_samples * F / (elapsed / args.steps) / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

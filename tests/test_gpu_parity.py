@@ -262,7 +262,7 @@ def test_step_count_matches_oracle(counter_clock):
                                np.flip(r.RotationMatrix, 0).astype(np.float32), np.float32([0, 3, 6]),
                                np.float32(0.9), np.float32([1, 1, 0]))
     out = torch.zeros(256 * 256 * 3, dtype=torch.float32, device="cuda")
-    steps = torch.zeros(8, dtype=torch.int64, device="cuda")
+    steps = torch.zeros(48, dtype=torch.int64, device="cuda")
     mex.render_device(r.objectHandle, ra, out.data_ptr(), None, steps.data_ptr())
     torch.cuda.synchronize()
     S = O.OracleSession()

@@ -21,18 +21,30 @@
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                          \
   }
 
-KERNEL(k_fma, asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_fma, asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(v[i]) : "v"(c), "v"(v[(i + 1) & 15])))
+KERNEL(k_fmac, asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(v[i]) : "v"(c), "v"(v[(i + 1) & 15])))
 KERNEL(k_mul, asm volatile("v_mul_f32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_addf, asm volatile("v_add_f32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_subf, asm volatile("v_sub_f32 %0, %1, %0" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_maxf, asm volatile("v_max_f32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_med3f, asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(v[i]) : "v"(c), "v"(v[(i + 1) & 15])))
 KERNEL(k_pkfma, asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(w[i]) : "v"((uint64_t)c)))
+KERNEL(k_pkmul, asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(w[i]) : "v"((uint64_t)c)))
+KERNEL(k_pkadd, asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(w[i]) : "v"((uint64_t)c)))
 KERNEL(k_addu, asm volatile("v_add_u32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_add3u, asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(v[i]) : "v"(c), "v"(v[(i + 1) & 15])))
+KERNEL(k_and, asm volatile("v_and_b32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
 KERNEL(k_mini, asm volatile("v_min_i32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_med3i, asm volatile("v_med3_i32 %0, %0, %1, %2" : "+v"(v[i]) : "v"(c), "v"(v[(i + 1) & 15])))
+KERNEL(k_mad24, asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(v[i]) : "v"(c), "v"(v[(i + 1) & 15])))
 KERNEL(k_cvt, asm volatile("v_cvt_i32_f32 %0, %0" : "+v"(v[i])))
+KERNEL(k_cvtf, asm volatile("v_cvt_f32_i32 %0, %0" : "+v"(v[i])))
 KERNEL(k_floor, asm volatile("v_floor_f32 %0, %0" : "+v"(v[i])))
+KERNEL(k_fract, asm volatile("v_fract_f32 %0, %0" : "+v"(v[i])))
 KERNEL(k_rndne, asm volatile("v_rndne_f32 %0, %0" : "+v"(v[i])))
-KERNEL(k_cnd, asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[i]) : "v"(c)))
+KERNEL(k_cnd, asm volatile("v_cmp_gt_f32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[i]) : "v"(c) : "vcc"))
 KERNEL(k_cmp, asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(v[i]), "v"(c) : "vcc"))
 KERNEL(k_mullo, asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(v[i]) : "v"(c)))
-KERNEL(k_mad64, asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %1, %0" : "+v"(w[i]) : "v"(c) : "s0", "s1"))
 KERNEL(k_lshl64, asm volatile("v_lshl_add_u64 %0, %0, 2, %0" : "+v"(w[i])))
 KERNEL(k_sqrt, asm volatile("v_sqrt_f32 %0, %0" : "+v"(v[i])))
 KERNEL(k_mov, asm volatile("v_mov_b32 %0, %1" : "=v"(v[i]) : "v"(v[(i + 1) & 15])))
@@ -46,10 +58,7 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   struct { const char *n; kfn f; } ks[] = {
-      {"v_fma_f32", k_fma}, {"v_mul_f32", k_mul}, {"v_pk_fma_f32", k_pkfma}, {"v_add_u32", k_addu},
-      {"v_min_i32", k_mini}, {"v_cvt_i32_f32", k_cvt}, {"v_floor_f32", k_floor}, {"v_rndne_f32", k_rndne},
-      {"v_cndmask_b32", k_cnd}, {"v_cmp_gt_f32", k_cmp}, {"v_mul_lo_u32", k_mullo}, {"v_mad_u64_u32", k_mad64},
-      {"v_lshl_add_u64", k_lshl64}, {"v_sqrt_f32", k_sqrt}, {"v_mov_b32", k_mov}, {"v_readlane_b32", k_readlane}};
+      {"v_fma_f32", k_fma}, {"v_fmac_f32", k_fmac}, {"v_mul_f32", k_mul}, {"v_add_f32", k_addf}, {"v_sub_f32", k_subf}, {"v_max_f32", k_maxf}, {"v_med3_f32", k_med3f}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_mul_f32", k_pkmul}, {"v_pk_add_f32", k_pkadd}, {"v_add_u32", k_addu}, {"v_add3_u32", k_add3u}, {"v_and_b32", k_and}, {"v_min_i32", k_mini}, {"v_med3_i32", k_med3i}, {"v_mad_u32_u24", k_mad24}, {"v_cvt_i32_f32", k_cvt}, {"v_cvt_f32_i32", k_cvtf}, {"v_floor_f32", k_floor}, {"v_fract_f32", k_fract}, {"v_rndne_f32", k_rndne}, {"v_cmp+v_cndmask", k_cnd}, {"v_cmp_gt_f32", k_cmp}, {"v_mul_lo_u32", k_mullo}, {"v_lshl_add_u64", k_lshl64}, {"v_sqrt_f32", k_sqrt}, {"v_mov_b32", k_mov}, {"v_readlane_b32", k_readlane}};
   int dev;
   hipGetDevice(&dev);
   hipDeviceProp_t p;

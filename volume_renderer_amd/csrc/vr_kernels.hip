@@ -45,38 +45,13 @@ __global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderP
     const int blk = lc / P.block_cols, within = lc - blk * P.block_cols;
     const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
 
-    // ray, volumeRender_kernel.cu:388-413
-    const float u = fmaf((float)x / P.fw, 2.f, -1.f);
-    const float v = fmaf(((float)y / P.fh) * 2.f, P.ratio, -P.ratio);
-    const f3 o = mk(P.eye[0], P.eye[1], P.eye[2]);
-    f3 du;
-    du.x = fmaf(P.focal, P.zdir[0], fmaf(v, P.ydir[0], u * P.nx_[0]));
-    du.y = fmaf(P.focal, P.zdir[1], fmaf(v, P.ydir[1], u * P.nx_[1]));
-    du.z = fmaf(P.focal, P.zdir[2], fmaf(v, P.ydir[2], u * P.nx_[2]));
-    const float inv = 1.f / sqrtf(dot3(du, du));
-    const f3 d = mk(du.x * inv, du.y * inv, du.z * inv);
-
-    // intersectBox, :155-199
+    f3 o, d;
+    float tnear, tfar;
+    const bool hit = ray_setup(P, x, y, o, d, tnear, tfar);  // volumeRender_kernel.cu:388-425
     const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
-    const f3 bmax = mk(-P.bmin[0], -P.bmin[1], -P.bmin[2]);
-    const f3 id = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
-    float tmin = ((id.x < 0.f ? bmax.x : bmin.x) - o.x) * id.x;
-    float tmax = ((id.x < 0.f ? bmin.x : bmax.x) - o.x) * id.x;
-    const float tymin = ((id.y < 0.f ? bmax.y : bmin.y) - o.y) * id.y;
-    const float tymax = ((id.y < 0.f ? bmin.y : bmax.y) - o.y) * id.y;
-    bool hit = !((tmin > tymax) || (tymin > tmax));
-    if (tymin > tmin) tmin = tymin;
-    if (tymax < tmax) tmax = tymax;
-    const float tzmin = ((id.z < 0.f ? bmax.z : bmin.z) - o.z) * id.z;
-    const float tzmax = ((id.z < 0.f ? bmin.z : bmax.z) - o.z) * id.z;
-    hit = hit && !((tmin > tzmax) || (tzmin > tmax));
-    if (tzmin > tmin) tmin = tzmin;
-    if (tzmax < tmax) tmax = tzmax;
 
     float sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f;
     if (hit) {
-      const float tnear = tmin < 0.f ? 0.f : tmin;
-      const float tfar = tmax;
       const float tstep = P.tstep, thr = P.thr;
       const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
       f3 pos = mk(fmaf(d.x, tnear, o.x), fmaf(d.y, tnear, o.y), fmaf(d.z, tnear, o.z));
@@ -135,42 +110,8 @@ __global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderP
               g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
                      tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
           }
-          // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
-          // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n
-          // below cancel when the view ray is parallel to n, and gamma then depends on every bit
-          // of n (an rsq here moved whole pixels by ~1%).
-          const float ginv = 1.f / sqrtf(dot3(g, g));
-          const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
           const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
-          const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
-          // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle
-          const float nlen = sqrtf(dot3(n, n));
-          const float alpha_n = acosf(dot3(n, li) / (nlen * sqrtf(dot3(li, li)))) / VR_PI;
-          const float dli = dot3(li, n);
-          const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-          const float liplen = sqrtf(dot3(lip, lip));
-          const Ax la = axis(alpha_n, P.lut.nx, P.lut.fnx);
-          for (int i = 0; i < P.num_lights; ++i) {
-            const DevLight L = P.lights[i];
-            const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);  // lightOut
-            const float beta = acosf(dot3(n, lo) / (nlen * sqrtf(dot3(lo, lo)))) / VR_PI;
-            const float dlo = dot3(lo, n);
-            const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-            const float gamma = acosf(dot3(lip, lop) / (liplen * sqrtf(dot3(lop, lop)))) / VR_PI;
-            float light = 0.f;
-            if (P.lut.p != nullptr) {
-              if (P.lut.one) {
-                const float q = P.lut.p[0];
-                light = fmaf(0.5f, q - q, q);
-              } else {
-                light = fetch<false>(P.lut, la, axis(beta, P.lut.ny, P.lut.fny), axis(gamma, P.lut.nz, P.lut.fnz));
-              }
-            }
-            const float rl = refl * light;
-            ir = fmaf(rl * L.cr, P.color[0], ir);
-            ig = fmaf(rl * L.cg, P.color[1], ig);
-            ib = fmaf(rl * L.cb, P.color[2], ib);
-          }
+          shade_lights(P, g, pos, o, refl, ir, ig, ib);
         }
         const float r = fmaf(eds, P.color[0], ir) * alpha;
         const float gg = fmaf(eds, P.color[1], ig) * alpha;

@@ -22,63 +22,67 @@
 
 namespace vr {
 
+// Per-lane march state carried across chunks.
+struct Ray {
+  f3 o, pos, step;
+  float t, tfar;
+  float sr, sg, sb, sa;
+  int32_t nsteps, nlit;
+  bool alive;
+};
+
+struct ChunkStats {
+  uint32_t staged, leap, fall, iter, lit;
+};
+
+// The chunked march of one wave.  NANCHK = false when every live ray of the wave has a finite
+// start position and step: all volume coordinates are then finite and the NaN -> 0 substitution
+// of the sampler is skipped (the LUT coordinates, which are NaN for a zero gradient, keep it).
 // MODE 0: no lights; 1: on-the-fly gradient from the staged emission texture (gem == em);
-// 2: lookup gradient (gx/gy/gz from global memory at the centre's axes when dims match).
-template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG>
-__global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
-  __shared__ float lds[4][VR_LDS_CAP];
-  int tx, ty;
-  if (!tile_of_block(P, tx, ty)) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float *L = lds[wave];
-  const int lc = tx * 16 + (wave & 1) * 8 + (lane >> 3);
-  const int y = ty * 16 + (wave >> 1) * 8 + (lane & 7);
-  const bool active = (lc < P.part_cols) && (y < P.height);
+// 2: lookup gradient (gx/gy/gz from global memory, at the centre's axes when SHARE2).
+template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK>
+__device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
   const DevTex &E = P.em;
-  int32_t nsteps = 0, nlit = 0;
-  uint32_t c_staged = 0, c_leap = 0, c_fall = 0;  // chunk statistics (COUNT builds)
-  uint32_t w_iter = 0, w_lit = 0;                  // wave sample iterations, of which with shading
-  float sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f;
-  f3 o = mk(0.f, 0.f, 0.f), d = mk(0.f, 0.f, 1.f), pos = o, step = o;
-  float t = 0.f, tfar = -1.f;
-  bool alive = false;
-  if (active) {
-    const int blk = lc / P.block_cols, within = lc - blk * P.block_cols;
-    const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
-    float tnear;
-    alive = ray_setup(P, x, y, o, d, tnear, tfar);
-    pos = mk(fmaf(d.x, tnear, o.x), fmaf(d.y, tnear, o.y), fmaf(d.z, tnear, o.z));
-    step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
-    t = tnear;
-  }
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
   const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
   const float tstep = P.tstep, thr = P.thr;
 
-  while (__any(alive)) {
+  while (__any(R.alive)) {
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
     int S;
-    bool staged;
+    bool staged, partial;
     Box B;
-    plan_chunk(P, alive, pos, step, t, tfar, S, staged, B);
+    int box_vol = 0;
+    plan_chunk(P, R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B, COUNT ? &box_vol : nullptr);
+    if (COUNT && lane == 0) {  // diagnostics: box volume of partial/failed chunks, S of staged ones
+      if (!staged || partial) atomicAdd(P.steps + 8 + min(box_vol >> 8, 31), 1ull);
+      else atomicAdd(P.steps + 40 + (S >= 32 ? 0 : (S >= 16 ? 1 : (S >= 8 ? 2 : 3))), 1ull);
+    }
     bool empty = false;
     if (staged) {
       const bool nonzero = stage_box(L, E, B, lane);  // always stage: the samples read the slot
-      empty = P.skip_empty && !nonzero;
+      empty = P.skip_empty && !partial && !nonzero;
     }
     __builtin_amdgcn_wave_barrier();
-    if (COUNT) ++(staged ? (empty ? c_leap : c_staged) : c_fall);
+    if (COUNT) ++(staged && !partial ? (empty ? C.leap : C.staged) : C.fall);
 
     if (empty) {
-      leap(P, S, alive, nsteps, t, tfar, pos, step);
+      leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
       continue;
     }
 
     // ---- S samples ---------------------------------------------------------------------------
-    for (int k = 0; k < S && alive; ++k) {
+    for (int k = 0; k < S && R.alive; ++k) {
+      const f3 pos = R.pos;
       const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
-      const Ax ax = axis(ps.x, E.nx, E.fnx), ay = axis(ps.y, E.ny, E.fny), az = axis(ps.z, E.nz, E.fnz);
-      const float em_s = fetch_em<BIG>(E, L, B, staged, ax, ay, az);
+      const Ax ax = axis<NANCHK>(ps.x, E.nx, E.fnx), ay = axis<NANCHK>(ps.y, E.ny, E.fny),
+               az = axis<NANCHK>(ps.z, E.nz, E.fnz);
+      // centre cell in the slot; the gradient taps below differ from it along one axis only
+      const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
+      const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
+      const int ayz = lz * B.pxy + ly * B.px;  // slot word of (0, ly, lz)
+      const int ac = ayz + lx;
+      const float em_s = fetch_at<BIG>(E, L, B, staged && inx && iny && inz, ac, ax, ay, az);
       const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
       const float e = P.fe * em_s;
       const float a = P.fa * ab_s;
@@ -91,11 +95,11 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
       float ir = 0.f, ig = 0.f, ib = 0.f;
       const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
       if (COUNT) {
-        ++w_iter;
-        w_lit += (MODE != 0 && __any(!skip)) ? 1u : 0u;
+        ++C.iter;
+        C.lit += (MODE != 0 && __any(!skip)) ? 1u : 0u;
       }
       if (MODE != 0 && !skip) {
-        if (COUNT) ++nlit;
+        if (COUNT) ++R.nlit;
         f3 g;
         if (MODE == 1 && (VR_ABLATE & 4)) {
           g = mk(ps.x, ps.y, em_s);
@@ -106,12 +110,21 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
           const float ym = ((pos.y - P.gstep[1]) - bmin.y) * bsc.y;
           const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
           const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
-          g.x = fetch_em<BIG>(E, L, B, staged, axis(xp, E.nx, E.fnx), ay, az) -
-                fetch_em<BIG>(E, L, B, staged, axis(xm, E.nx, E.fnx), ay, az);
-          g.y = fetch_em<BIG>(E, L, B, staged, ax, axis(yp, E.ny, E.fny), az) -
-                fetch_em<BIG>(E, L, B, staged, ax, axis(ym, E.ny, E.fny), az);
-          g.z = fetch_em<BIG>(E, L, B, staged, ax, ay, axis(zp, E.nz, E.fnz)) -
-                fetch_em<BIG>(E, L, B, staged, ax, ay, axis(zm, E.nz, E.fnz));
+          const bool syz = staged && iny && inz, sxz = staged && inx && inz, sxy = staged && inx && iny;
+          const Ax axp = axis<NANCHK>(xp, E.nx, E.fnx), axm = axis<NANCHK>(xm, E.nx, E.fnx);
+          const int lxp = slot_coord(axp.i, B.rx), lxm = slot_coord(axm.i, B.rx);
+          g.x = fetch_at<BIG>(E, L, B, syz && in_box(lxp, B.ex), ayz + lxp, axp, ay, az) -
+                fetch_at<BIG>(E, L, B, syz && in_box(lxm, B.ex), ayz + lxm, axm, ay, az);
+          const Ax ayp = axis<NANCHK>(yp, E.ny, E.fny), aym = axis<NANCHK>(ym, E.ny, E.fny);
+          const int lyp = slot_coord(ayp.i, B.ry), lym = slot_coord(aym.i, B.ry);
+          const int axz = lz * B.pxy + lx;
+          g.y = fetch_at<BIG>(E, L, B, sxz && in_box(lyp, B.ey), axz + lyp * B.px, ax, ayp, az) -
+                fetch_at<BIG>(E, L, B, sxz && in_box(lym, B.ey), axz + lym * B.px, ax, aym, az);
+          const Ax azp = axis<NANCHK>(zp, E.nz, E.fnz), azm = axis<NANCHK>(zm, E.nz, E.fnz);
+          const int lzp = slot_coord(azp.i, B.rz), lzm = slot_coord(azm.i, B.rz);
+          const int axy = ly * B.px + lx;
+          g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
+                fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
           g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
         } else if (SHARE2) {
           g = mk(fetch<BIG>(P.gx, ax, ay, az), fetch<BIG>(P.gy, ax, ay, az), fetch<BIG>(P.gz, ax, ay, az));
@@ -120,36 +133,78 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
                  tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
         }
         const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
-        shade_lights(P, g, pos, o, refl, ir, ig, ib);
+        shade_lights(P, g, pos, R.o, refl, ir, ig, ib);
       }
       const float r = fmaf(eds, P.color[0], ir) * alpha;
       const float gg = fmaf(eds, P.color[1], ig) * alpha;
       const float b = fmaf(eds, P.color[2], ib) * alpha;
-      const float om = 1.f - sa;
-      sr = fmaf(om, r, sr);
-      sg = fmaf(om, gg, sg);
-      sb = fmaf(om, b, sb);
-      sa = fmaf(om, alpha, sa);
-      ++nsteps;
-      if (sa > thr || nsteps >= P.max_steps) {
-        alive = false;
+      const float om = 1.f - R.sa;
+      R.sr = fmaf(om, r, R.sr);
+      R.sg = fmaf(om, gg, R.sg);
+      R.sb = fmaf(om, b, R.sb);
+      R.sa = fmaf(om, alpha, R.sa);
+      ++R.nsteps;
+      if (R.sa > thr || R.nsteps >= P.max_steps) {
+        R.alive = false;
       } else {
-        t += tstep;
-        if (t > tfar) alive = false;
-        else pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
+        R.t += tstep;
+        if (R.t > R.tfar) R.alive = false;
+        else R.pos = mk(pos.x + R.step.x, pos.y + R.step.y, pos.z + R.step.z);
       }
     }
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+__device__ __forceinline__ bool finite3(const f3 &v) {
+  return fabsf(v.x) <= 3.4e38f && fabsf(v.y) <= 3.4e38f && fabsf(v.z) <= 3.4e38f;
+}
+
+template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG>
+__global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
+  __shared__ float lds[4][VR_LDS_CAP];
+  int tx, ty;
+  if (!tile_of_block(P, tx, ty)) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float *L = lds[wave];
+  const int lc = tx * 16 + (wave & 1) * 8 + (lane >> 3);
+  const int y = ty * 16 + (wave >> 1) * 8 + (lane & 7);
+  const bool active = (lc < P.part_cols) && (y < P.height);
+  Ray R;
+  R.o = mk(0.f, 0.f, 0.f);
+  R.pos = R.o;
+  R.step = R.o;
+  R.t = 0.f;
+  R.tfar = -1.f;
+  R.sr = R.sg = R.sb = R.sa = 0.f;
+  R.nsteps = R.nlit = 0;
+  R.alive = false;
+  ChunkStats C{0, 0, 0, 0, 0};
+  if (active) {
+    const int blk = lc / P.block_cols, within = lc - blk * P.block_cols;
+    const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
+    f3 d;
+    float tnear;
+    R.alive = ray_setup(P, x, y, R.o, d, tnear, R.tfar);
+    R.pos = mk(fmaf(d.x, tnear, R.o.x), fmaf(d.y, tnear, R.o.y), fmaf(d.z, tnear, R.o.z));
+    R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
+    R.t = tnear;
+  }
+  // every coordinate the march forms from a finite start and step is finite
+  if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, false>(P, L, lane, R, C);
+  else
+    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, true>(P, L, lane, R, C);
+
   if (active) {
     const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
     const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
-    P.out[kk] = sr;
-    P.out[kk + plane] = sg;
-    P.out[kk + 2 * plane] = sb;
+    P.out[kk] = R.sr;
+    P.out[kk + plane] = R.sg;
+    P.out[kk + 2 * plane] = R.sb;
   }
   if (COUNT) {
-    unsigned long long s = (unsigned long long)nsteps, l = (unsigned long long)nlit;
+    unsigned long long s = (unsigned long long)R.nsteps, l = (unsigned long long)R.nlit;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       s += __shfl_xor(s, off, 64);
@@ -158,11 +213,11 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
     if (lane == 0 && s) atomicAdd(P.steps, s);
     if (lane == 0 && l) atomicAdd(P.steps + 1, l);
     if (lane == 0) {  // per-wave chunk counts (uniform values)
-      atomicAdd(P.steps + 2, (unsigned long long)c_staged);
-      atomicAdd(P.steps + 3, (unsigned long long)c_leap);
-      atomicAdd(P.steps + 4, (unsigned long long)c_fall);
-      atomicAdd(P.steps + 5, (unsigned long long)w_iter);
-      atomicAdd(P.steps + 6, (unsigned long long)w_lit);
+      atomicAdd(P.steps + 2, (unsigned long long)C.staged);
+      atomicAdd(P.steps + 3, (unsigned long long)C.leap);
+      atomicAdd(P.steps + 4, (unsigned long long)C.fall);
+      atomicAdd(P.steps + 5, (unsigned long long)C.iter);
+      atomicAdd(P.steps + 6, (unsigned long long)C.lit);
     }
   }
 }

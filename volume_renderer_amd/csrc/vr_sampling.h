@@ -21,18 +21,38 @@ __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a
 typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
 
 // One axis of the linear-filter address computation (normalized coords, clamp addressing):
-// pair base i' = clamp(floor(c*n - 0.5), -1, n-1) and the 8-bit weight.
+// pair base i' = clamp(floor(c*n - 0.5), -1, n-1) and the 8-bit weight.  The clamp runs on the
+// float floor before the conversion (one v_med3 instead of v_max + v_min: the same integer for
+// every floor value, +-inf included).  NANCHK = false skips the NaN -> 0 substitution where the
+// caller has proven the coordinate finite.
 struct Ax {
   int i;
   float w;
 };
+template <bool NANCHK = true>
 __device__ __forceinline__ Ax axis(float c, int n, float fn) {
-  c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
+  if (NANCHK) c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
   const float xb = c * fn - 0.5f;
   const float fl = floorf(xb);
   const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
-  const int i = (int)fl;
-  return Ax{min(max(i, -1), n - 1), w};
+  (void)n;
+  return Ax{(int)__builtin_amdgcn_fmed3f(fl, -1.f, fn - 1.f), w};
+}
+
+// Correctly rounded sqrtf for x >= 0, NaN or +inf.  The device library's sqrtf scales inputs
+// below 2^-96 and patches +-0 / inf by class; for x == 0 or x >= 2^-96 its remaining steps (the
+// hardware root corrected by one ulp either way from two fma residuals) give the identical result
+// on their own, so when every lane of the wave is in that range the scaling is skipped.
+__device__ __forceinline__ float sqrt_cr(float x) {
+  const uint32_t u = __float_as_uint(x);
+  if (__builtin_expect(__all(u - 1u >= 0x0f7fffffu), 1)) {  // x == 0, x >= 2^-96 (or x < 0, NaN)
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = fmaf(-sm, s, x), rp = fmaf(-sp, s, x);
+    const float r = (rm <= 0.f) ? sm : s;
+    return (rp > 0.f) ? sp : r;
+  }
+  return sqrtf(x);
 }
 
 __device__ __forceinline__ float lerp(float a, float b, float w) { return fmaf(w, b - a, a); }
@@ -106,7 +126,7 @@ __device__ __forceinline__ bool ray_setup(const RenderParams &P, int x, int y, f
   du.x = fmaf(P.focal, P.zdir[0], fmaf(v, P.ydir[0], u * P.nx_[0]));
   du.y = fmaf(P.focal, P.zdir[1], fmaf(v, P.ydir[1], u * P.nx_[1]));
   du.z = fmaf(P.focal, P.zdir[2], fmaf(v, P.ydir[2], u * P.nx_[2]));
-  const float inv = 1.f / sqrtf(dot3(du, du));
+  const float inv = 1.f / sqrt_cr(dot3(du, du));
   d = mk(du.x * inv, du.y * inv, du.z * inv);
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
   const f3 bmax = mk(-P.bmin[0], -P.bmin[1], -P.bmin[2]);
@@ -149,19 +169,19 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
   // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
   // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n below
   // cancel when the view ray is parallel to n, and gamma then depends on every bit of n.
-  const float ginv = 1.f / sqrtf(dot3(g, g));
+  const float ginv = 1.f / sqrt_cr(dot3(g, g));
   const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
   const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
   // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle
-  const float nlen = sqrtf(dot3(n, n));
+  const float nlen = sqrt_cr(dot3(n, n));
 #if VR_ABLATE & 2
   const float alpha_n = dot3(n, li) * 0.1f;
 #else
-  const float alpha_n = divpi(acosf(dot3(n, li) / (nlen * sqrtf(dot3(li, li)))));
+  const float alpha_n = divpi(acosf(dot3(n, li) / (nlen * sqrt_cr(dot3(li, li)))));
 #endif
   const float dli = dot3(li, n);
   const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-  const float liplen = sqrtf(dot3(lip, lip));
+  const float liplen = sqrt_cr(dot3(lip, lip));
   const Ax la = axis(alpha_n, P.lut.nx, P.lut.fnx);
   for (int i = 0; i < P.num_lights; ++i) {
     const DevLight L = P.lights[i];
@@ -169,10 +189,10 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #if VR_ABLATE & 2
     const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
 #else
-    const float beta = divpi(acosf(dot3(n, lo) / (nlen * sqrtf(dot3(lo, lo)))));
+    const float beta = divpi(acosf(dot3(n, lo) / (nlen * sqrt_cr(dot3(lo, lo)))));
     const float dlo = dot3(lo, n);
     const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-    const float gamma = divpi(acosf(dot3(lip, lop) / (liplen * sqrtf(dot3(lop, lop)))));
+    const float gamma = divpi(acosf(dot3(lip, lop) / (liplen * sqrt_cr(dot3(lop, lop)))));
 #endif
     float light = 0.f;
 #if VR_ABLATE & 1

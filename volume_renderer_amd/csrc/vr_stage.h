@@ -43,24 +43,37 @@ struct Box {
   int rx, ry, rz, ex, ey, ez, px, pxy;
 };
 
-// Trilinear fetch of the staged emission texture: LDS when the 2x2x2 cell lies in the box.
+// Trilinear interpolation of the staged cell whose (x, y, z) = (0, 0, 0) corner is slot word a.
+__device__ __forceinline__ float lds_tri(const float *L, const Box &B, int a, float wx, float wy, float wz) {
+  const float c00 = lerp(L[a], L[a + 1], wx);
+  const float c10 = lerp(L[a + B.px], L[a + B.px + 1], wx);
+  const float c01 = lerp(L[a + B.pxy], L[a + B.pxy + 1], wx);
+  const float c11 = lerp(L[a + B.pxy + B.px], L[a + B.pxy + B.px + 1], wx);
+  const float c0 = lerp(c00, c10, wy), c1 = lerp(c01, c11, wy);
+  return lerp(c0, c1, wz);
+}
+
+// Slot coordinates of a tap pair base and whether the cell [l, l+1] lies in the box along it.
+__device__ __forceinline__ int slot_coord(int i, int r) { return i + 1 - r; }
+__device__ __forceinline__ bool in_box(int l, int e) {
+  return (VR_ABLATE & 16) || (unsigned)l < (unsigned)(e - 1);
+}
+
+// Trilinear fetch of the staged emission texture: the slot when the 2x2x2 cell lies in the box
+// (`in`, with slot word `a`), global memory otherwise -- the same interpolation either way.
+template <bool BIG>
+__device__ __forceinline__ float fetch_at(const DevTex &t, const float *L, const Box &B, bool in, int a,
+                                          const Ax &ax, const Ax &ay, const Ax &az) {
+  if (in) return lds_tri(L, B, a, ax.w, ay.w, az.w);
+  return fetch<BIG>(t, ax, ay, az);
+}
+
 template <bool BIG>
 __device__ __forceinline__ float fetch_em(const DevTex &t, const float *L, const Box &B, bool staged,
                                           const Ax &ax, const Ax &ay, const Ax &az) {
-  if (staged) {
-    const int lx = ax.i + 1 - B.rx, ly = ay.i + 1 - B.ry, lz = az.i + 1 - B.rz;
-    if ((VR_ABLATE & 16) || ((unsigned)lx < (unsigned)(B.ex - 1) && (unsigned)ly < (unsigned)(B.ey - 1) &&
-                             (unsigned)lz < (unsigned)(B.ez - 1))) {
-      const int a = lz * B.pxy + ly * B.px + lx;
-      const float c00 = lerp(L[a], L[a + 1], ax.w);
-      const float c10 = lerp(L[a + B.px], L[a + B.px + 1], ax.w);
-      const float c01 = lerp(L[a + B.pxy], L[a + B.pxy + 1], ax.w);
-      const float c11 = lerp(L[a + B.pxy + B.px], L[a + B.pxy + B.px + 1], ax.w);
-      const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
-      return lerp(c0, c1, az.w);
-    }
-  }
-  return fetch<BIG>(t, ax, ay, az);
+  const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
+  const bool in = staged && in_box(lx, B.ex) && in_box(ly, B.ey) && in_box(lz, B.ez);
+  return fetch_at<BIG>(t, L, B, in, lz * B.pxy + ly * B.px + lx, ax, ay, az);
 }
 
 // Padded index range [lo, hi] (inclusive) of the tap pairs of one axis for a coordinate range.
@@ -116,20 +129,28 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
 }
 
 
+#ifndef VR_PARTIAL
+#define VR_PARTIAL 1     // stage a centred sub-box when no whole box fits (taps outside: global)
+#endif
+
 // Chunk set-up: the box of every tap the wave's live rays take in their next S samples, S halved
-// (up to VR_ATTEMPTS tries) until the box fits the slot; staged == false: march 8 samples from
-// global memory.  The predicted end position fma(step, k, pos) is bounded against the k
-// sequentially rounded additions by RenderParams::tap_off.
+// (up to VR_ATTEMPTS tries) until the box fits the slot.  When none fits, the last box is shrunk
+// about its centre until it does (partial = true): taps outside it read global memory (the
+// fetch checks every cell against the box), and the chunk may not be leaped.  The predicted end
+// position fma(step, k, pos) is bounded against the k sequentially rounded additions by
+// RenderParams::tap_off.
 __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, const f3 &pos, const f3 &step,
-                                           float t, float tfar, int &S, bool &staged, Box &B) {
+                                           float t, float tfar, int &S, bool &staged, bool &partial, Box &B,
+                                           int *vol_out = nullptr) {
   const DevTex &E = P.em;
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
   const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
   const float tstep = P.tstep;
   S = VR_CHUNK;
   staged = false;
+  partial = false;
   B = Box{0, 0, 0, 1, 1, 1, 1, 1};
-  for (int attempt = 0; attempt < VR_ATTEMPTS; ++attempt, S >>= 1) {
+  for (int attempt = 0;; ++attempt) {
     int lo[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, hi[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
     if (alive) {
       const float rem = (tfar - t) / tstep;  // samples left before the exit test fires
@@ -151,12 +172,35 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
     B.ez = wave_max(hi[2]) - B.rz + 1;
     B.px = VR_ODD_PITCH ? (B.ex | 1) : B.ex;
     B.pxy = VR_ODD_PITCH ? ((B.px * B.ey) | 1) : B.px * B.ey;
-    if (B.ex > 0 && B.ey > 0 && B.ez > 0 && B.pxy * B.ez <= VR_LDS_CAP) {
+    if (vol_out) *vol_out = B.pxy * B.ez;
+    if (B.ex <= 0 || B.ey <= 0 || B.ez <= 0) return;  // no live ray
+    if (B.pxy * B.ez <= VR_LDS_CAP) {
       staged = true;
       return;
     }
-    if (attempt == VR_ATTEMPTS - 1) S = 8;  // no box fits: march 8 samples from global memory
+    if (attempt == VR_ATTEMPTS - 1) break;
+    S >>= 1;
   }
+#if VR_PARTIAL
+  // shrink the largest extent about the centre until the sub-box fits (wave-uniform scalars)
+  int e[3] = {B.ex, B.ey, B.ez}, r[3] = {B.rx, B.ry, B.rz};
+  while (e[0] * e[1] * e[2] > VR_LDS_CAP) {
+    const int a = (e[0] >= e[1] && e[0] >= e[2]) ? 0 : (e[1] >= e[2] ? 1 : 2);
+    if (e[a] <= 2) break;
+    r[a] += e[a] & 1;  // trim alternately from the low and the high side
+    --e[a];
+  }
+  B.rx = r[0]; B.ry = r[1]; B.rz = r[2];
+  B.ex = e[0]; B.ey = e[1]; B.ez = e[2];
+  B.px = B.ex;
+  B.pxy = B.ex * B.ey;
+  if (B.pxy * B.ez <= VR_LDS_CAP) {
+    staged = true;
+    partial = true;
+    return;
+  }
+#endif
+  S >>= 1;  // no box fits: march S/2 samples from global memory
 }
 
 // The empty-chunk leap: every tap of the chunk lies in the staged all-zero box, so each sample has
