@@ -3,7 +3,7 @@
 # usage: tools/ablate_build.sh NAME "-DFLAG=.. -DFLAG2=.."
 set -e
 cd "$(dirname "$0")/../volume_renderer_amd/csrc"
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $2"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize $2"
 mkdir -p ../../build_ab/$1
 for f in vr_capi vr_kernels vr_march; do hipcc $F -c $f.hip -o ../../build_ab/$1/$f.o; done
 hipcc --offload-arch=gfx950 -shared -o ../../build_ab/libvrhip_$1.so ../../build_ab/$1/*.o

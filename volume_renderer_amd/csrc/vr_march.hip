@@ -60,7 +60,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     }
     bool empty = false;
     if (staged) {
-      const bool nonzero = stage_box(L, E, B, lane);  // always stage: the samples read the slot
+      const bool nonzero = stage_box<BIG>(L, E, B, lane);  // always stage: the samples read the slot
       empty = P.skip_empty && !partial && !nonzero;
     }
     __builtin_amdgcn_wave_barrier();

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <type_traits>
 
 #include "vr_device.h"
 #include "vr_sampling.h"
@@ -86,9 +87,9 @@ __device__ __forceinline__ void axis_range(float c0, float c1, float off, int n,
   hi = min(max(b, -1), n - 1) + 2;
 }
 
-// Copy box B of the apron volume into the wave's LDS slot (row-major, x fastest).  Returns
-// whether any staged voxel is non-zero (NaN counts as non-zero), for the whole wave.
-__device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &B, int lane) {
+// Element-wise copy of box B into the slot (any box shape and pitch).  Returns whether any
+// staged voxel is non-zero (NaN counts as non-zero), for the whole wave.
+__device__ __forceinline__ bool stage_box_elems(float *L, const DevTex &t, const Box &B, int lane) {
   bool nz = false;
   const uint32_t ex = (uint32_t)B.ex, ey = (uint32_t)B.ey;
   const uint32_t V = ex * ey * (uint32_t)B.ez;
@@ -128,6 +129,58 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
   return __any(nz);
 }
 
+
+// Copy box B of the apron volume into the wave's LDS slot (row-major, x fastest).  A wave pass
+// moves 64 / ex whole rows (lane -> (row slot, x)); row offsets advance incrementally, relative to
+// a wave-uniform base pointer, so a pass costs a handful of adds instead of per-element 64-bit
+// index products.  Returns whether any staged voxel is non-zero (NaN counts as non-zero), for
+// the whole wave.
+template <bool BIG>
+__device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &B, int lane) {
+  const int ex = B.ex, ey = B.ey;
+  if (ex > 64 || B.pxy != B.px * ey) return stage_box_elems(L, t, B, lane);
+  if (!BIG && (uint64_t)t.pxy * (uint64_t)B.ez * 4u >= 0xFFFFFFFFull)  // 32-bit byte offsets overflow
+    return stage_box_elems(L, t, B, lane);
+  typedef typename std::conditional<BIG, uint64_t, uint32_t>::type off_t;
+  const int per = 64 / ex;  // rows per pass (wave-uniform)
+  const int rr = lane / ex, xr = lane - rr * ex;
+  const int rows = ey * B.ez;
+  const int n = rr < per ? (rows - rr + per - 1) / per : 0;  // passes with a row for this lane
+  int y = rr % ey;
+  const int z = rr / ey;
+  const char *base = reinterpret_cast<const char *>(
+      t.p + ((uint64_t)B.rz * t.pxy + (uint64_t)B.ry * t.px + (uint64_t)B.rx));  // uniform
+  off_t g = ((off_t)z * t.pxy + (off_t)y * t.px + (off_t)xr) * 4u;               // bytes
+  const off_t g_row = (off_t)per * t.px * 4u;
+  const off_t g_wrap = ((off_t)t.pxy - (off_t)ey * t.px) * 4u;
+  int l = rr * B.px + xr;  // slot word (pxy == px * ey: row r starts at r * px)
+  const int l_row = per * B.px;
+  uint32_t acc = 0;
+  for (int k0 = 0; k0 < n; k0 += 4) {
+    float v[4];
+    int li[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      li[j] = l;
+      if (k0 + j < n) v[j] = *reinterpret_cast<const float *>(base + g);
+      l += l_row;
+      g += g_row;
+      y += per;
+      while (y >= ey) {
+        y -= ey;
+        g += g_wrap;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (k0 + j < n) {
+        L[li[j]] = v[j];
+        acc |= __float_as_uint(v[j]) & 0x7fffffffu;
+      }
+    }
+  }
+  return __any(acc != 0u);
+}
 
 #ifndef VR_PARTIAL
 #define VR_PARTIAL 1     // stage a centred sub-box when no whole box fits (taps outside: global)
