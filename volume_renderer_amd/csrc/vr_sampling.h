@@ -78,6 +78,23 @@ __device__ __forceinline__ float fetch(const DevTex &t, const Ax &ax, const Ax &
   return lerp(c0, c1, az.w);
 }
 
+// Trilinear fetch from a texture smaller than 4 GiB (the illumination LUT): 32-bit byte offsets
+// from the wave-uniform base, so the four row loads use scalar-base addressing and no 64-bit
+// vector pointer arithmetic.  Same interpolation as fetch().
+__device__ __forceinline__ float fetch_small(const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
+  const uint32_t o = (((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1)) * 4u;
+  const uint32_t px4 = t.px * 4u, pxy4 = t.pxy * 4u;
+  const char *b = reinterpret_cast<const char *>(t.p);
+  const f2a4 r00 = *reinterpret_cast<const f2a4 *>(b + o);
+  const f2a4 r10 = *reinterpret_cast<const f2a4 *>(b + (o + px4));
+  const f2a4 r01 = *reinterpret_cast<const f2a4 *>(b + (o + pxy4));
+  const f2a4 r11 = *reinterpret_cast<const f2a4 *>(b + (o + pxy4 + px4));
+  const float c00 = lerp(r00.x, r00.y, ax.w), c10 = lerp(r10.x, r10.y, ax.w);
+  const float c01 = lerp(r01.x, r01.y, ax.w), c11 = lerp(r11.x, r11.y, ax.w);
+  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
+  return lerp(c0, c1, az.w);
+}
+
 // tex3D on any texture state (unbound -> 0, 1x1x1 -> single voxel through the same lerp algebra).
 template <bool BIG>
 __device__ __forceinline__ float tex3d(const DevTex &t, float x, float y, float z) {
@@ -155,6 +172,24 @@ __device__ __forceinline__ bool ray_setup(const RenderParams &P, int x, int y, f
                      // 16 no staged-box check
 #endif
 
+// a / b for the arguments of the angle acosf calls, bit-identical to IEEE a / b wherever it can
+// matter: the compiler's correctly rounded sequence (Newton-refined reciprocal, two residual
+// corrections) without its v_div_scale / v_div_fixup range handling, which is the identity for
+// 2^-40 <= |b| <= 2^40 and |a| <= 2^40 (tools/microbench: 2^33 random pairs, 0 mismatches).  Here
+// |a| <= |b| (Cauchy-Schwarz, up to rounding), and a tiny quotient gives acosf == pi/2 however it
+// rounds, so only b is tested; a wave with any other lane takes '/'.
+__device__ __forceinline__ float div_acos_arg(float a, float b) {
+  const uint32_t ub = __float_as_uint(b) & 0x7fffffffu;
+  if (__builtin_expect(__all(ub - 0x2b800000u <= 0x28000000u), 1)) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float y1 = fmaf(fmaf(-b, y0, 1.f), y0, y0);
+    const float q0 = a * y1;
+    const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
+    return fmaf(fmaf(-b, q1, a), y1, q1);
+  }
+  return a / b;
+}
+
 // x / pi, correctly rounded, for x = 0, NaN or x >= 2^-100 -- the range of acosf: x * RN(1/pi)
 // corrected by one fma residual step (3 VALU instead of the 12 of a general IEEE divide).  Equal to
 // the IEEE quotient for every such fp32 x (exhaustive check: tools/microbench/divpi_check.c).
@@ -177,7 +212,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #if VR_ABLATE & 2
   const float alpha_n = dot3(n, li) * 0.1f;
 #else
-  const float alpha_n = divpi(acosf(dot3(n, li) / (nlen * sqrt_cr(dot3(li, li)))));
+  const float alpha_n = divpi(acosf(div_acos_arg(dot3(n, li), nlen * sqrt_cr(dot3(li, li)))));
 #endif
   const float dli = dot3(li, n);
   const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
@@ -189,10 +224,10 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #if VR_ABLATE & 2
     const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
 #else
-    const float beta = divpi(acosf(dot3(n, lo) / (nlen * sqrt_cr(dot3(lo, lo)))));
+    const float beta = divpi(acosf(div_acos_arg(dot3(n, lo), nlen * sqrt_cr(dot3(lo, lo)))));
     const float dlo = dot3(lo, n);
     const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-    const float gamma = divpi(acosf(dot3(lip, lop) / (liplen * sqrt_cr(dot3(lop, lop)))));
+    const float gamma = divpi(acosf(div_acos_arg(dot3(lip, lop), liplen * sqrt_cr(dot3(lop, lop)))));
 #endif
     float light = 0.f;
 #if VR_ABLATE & 1
@@ -205,7 +240,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
         const float q = P.lut.p[0];
         light = fmaf(0.5f, q - q, q);
       } else {
-        light = fetch<false>(P.lut, la, axis(beta, P.lut.ny, P.lut.fny), axis(gamma, P.lut.nz, P.lut.fnz));
+        light = fetch_small(P.lut, la, axis(beta, P.lut.ny, P.lut.fny), axis(gamma, P.lut.nz, P.lut.fnz));
       }
     }
     const float rl = refl * light;
