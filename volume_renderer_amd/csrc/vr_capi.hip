@@ -335,6 +335,11 @@ vr::DevTex dev_tex(const BufPtr &b) {
     t.fny = (float)t.ny;
     t.fnz = (float)t.nz;
     t.one = (t.nx == 1 && t.ny == 1 && t.nz == 1);
+    const uint64_t padded = (b->dims[0] + 2) * (b->dims[1] + 2) * (b->dims[2] + 2);
+    t.small = padded < (1ull << 22);
+    t.fpx4 = 4.f * (float)t.px;
+    t.fpxy4 = 4.f * (float)t.pxy;
+    t.fbase4 = 4.f * (float)(t.pxy + t.px + 1);
   }
   return t;
 }

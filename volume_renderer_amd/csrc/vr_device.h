@@ -19,6 +19,8 @@ struct DevTex {
   uint32_t pxy;   // (nx + 2) * (ny + 2) (plane pitch, elements)
   float fnx, fny, fnz;  // (float)n for the coordinate transform
   int32_t one;    // 1x1x1 volume: every fetch is the single voxel
+  int32_t small;  // padded size < 2^22 voxels: byte offsets are exact in fp32 (fetch_small)
+  float fpx4, fpxy4, fbase4;  // 4*px, 4*pxy, 4*(pxy+px+1): byte-offset terms for fetch_small
 };
 
 // One light in kernel order (position reversed from MATLAB, render.cpp:167-168).

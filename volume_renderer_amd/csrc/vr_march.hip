@@ -75,8 +75,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     for (int k = 0; k < S && R.alive; ++k) {
       const f3 pos = R.pos;
       const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
-      const Ax ax = axis<NANCHK>(ps.x, E.nx, E.fnx), ay = axis<NANCHK>(ps.y, E.ny, E.fny),
-               az = axis<NANCHK>(ps.z, E.nz, E.fnz);
+      // unclamped axes (axis_raw): exact on the LDS path, clamped by fetch_at on the global one
+      const Ax ax = axis_raw<NANCHK>(ps.x, E.fnx), ay = axis_raw<NANCHK>(ps.y, E.fny),
+               az = axis_raw<NANCHK>(ps.z, E.fnz);
       // centre cell in the slot; the gradient taps below differ from it along one axis only
       const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
       const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
@@ -111,23 +112,24 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
           const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
           const bool syz = staged && iny && inz, sxz = staged && inx && inz, sxy = staged && inx && iny;
-          const Ax axp = axis<NANCHK>(xp, E.nx, E.fnx), axm = axis<NANCHK>(xm, E.nx, E.fnx);
+          const Ax axp = axis_raw<NANCHK>(xp, E.fnx), axm = axis_raw<NANCHK>(xm, E.fnx);
           const int lxp = slot_coord(axp.i, B.rx), lxm = slot_coord(axm.i, B.rx);
           g.x = fetch_at<BIG>(E, L, B, syz && in_box(lxp, B.ex), ayz + lxp, axp, ay, az) -
                 fetch_at<BIG>(E, L, B, syz && in_box(lxm, B.ex), ayz + lxm, axm, ay, az);
-          const Ax ayp = axis<NANCHK>(yp, E.ny, E.fny), aym = axis<NANCHK>(ym, E.ny, E.fny);
+          const Ax ayp = axis_raw<NANCHK>(yp, E.fny), aym = axis_raw<NANCHK>(ym, E.fny);
           const int lyp = slot_coord(ayp.i, B.ry), lym = slot_coord(aym.i, B.ry);
           const int axz = lz * B.pxy + lx;
           g.y = fetch_at<BIG>(E, L, B, sxz && in_box(lyp, B.ey), axz + lyp * B.px, ax, ayp, az) -
                 fetch_at<BIG>(E, L, B, sxz && in_box(lym, B.ey), axz + lym * B.px, ax, aym, az);
-          const Ax azp = axis<NANCHK>(zp, E.nz, E.fnz), azm = axis<NANCHK>(zm, E.nz, E.fnz);
+          const Ax azp = axis_raw<NANCHK>(zp, E.fnz), azm = axis_raw<NANCHK>(zm, E.fnz);
           const int lzp = slot_coord(azp.i, B.rz), lzm = slot_coord(azm.i, B.rz);
           const int axy = ly * B.px + lx;
           g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
                 fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
           g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
         } else if (SHARE2) {
-          g = mk(fetch<BIG>(P.gx, ax, ay, az), fetch<BIG>(P.gy, ax, ay, az), fetch<BIG>(P.gz, ax, ay, az));
+          const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
+          g = mk(fetch<BIG>(P.gx, cx, cy, cz), fetch<BIG>(P.gy, cx, cy, cz), fetch<BIG>(P.gz, cx, cy, cz));
         } else {
           g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
                  tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));

@@ -39,6 +39,19 @@ __device__ __forceinline__ Ax axis(float c, int n, float fn) {
   return Ax{(int)__builtin_amdgcn_fmed3f(fl, -1.f, fn - 1.f), w};
 }
 
+// The pair base without the clamp, and the weight.  Wherever the cell [i, i+1] lies inside a
+// staged box the clamp is the identity (box coordinates are clamped indices: an index below -1 or
+// above n-1 cannot fall in the box), so the LDS path uses this and the global path clamps.
+template <bool NANCHK = true>
+__device__ __forceinline__ Ax axis_raw(float c, float fn) {
+  if (NANCHK) c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
+  const float xb = c * fn - 0.5f;
+  const float fl = floorf(xb);
+  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
+  return Ax{(int)fl, w};
+}
+__device__ __forceinline__ Ax clamp_ax(const Ax &a, int n) { return Ax{min(max(a.i, -1), n - 1), a.w}; }
+
 // Correctly rounded sqrtf for x >= 0, NaN or +inf.  The device library's sqrtf scales inputs
 // below 2^-96 and patches +-0 / inf by class; for x == 0 or x >= 2^-96 its remaining steps (the
 // hardware root corrected by one ulp either way from two fma residuals) give the identical result
@@ -78,11 +91,26 @@ __device__ __forceinline__ float fetch(const DevTex &t, const Ax &ax, const Ax &
   return lerp(c0, c1, az.w);
 }
 
-// Trilinear fetch from a texture smaller than 4 GiB (the illumination LUT): 32-bit byte offsets
-// from the wave-uniform base, so the four row loads use scalar-base addressing and no 64-bit
-// vector pointer arithmetic.  Same interpolation as fetch().
-__device__ __forceinline__ float fetch_small(const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
-  const uint32_t o = (((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1)) * 4u;
+// Axis of a texture whose offsets are formed in fp32 (fetch_small): the clamped floor kept as a
+// float (the same value axis() converts) and the weight.
+struct AxF {
+  float fl;
+  float w;
+};
+__device__ __forceinline__ AxF axis_f(float c, float fn) {
+  c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
+  const float xb = c * fn - 0.5f;
+  const float fl = floorf(xb);
+  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
+  return AxF{__builtin_amdgcn_fmed3f(fl, -1.f, fn - 1.f), w};
+}
+
+// Trilinear fetch from a texture of fewer than 2^22 padded voxels (the illumination LUT): the
+// byte offset 4*((i'z+1)*pxy + (i'y+1)*px + (i'x+1)) is an integer below 2^24, so it is formed
+// exactly with three fmas on the float floors and converted once; the four row loads then use
+// the wave-uniform base with 32-bit offsets.  Same interpolation as fetch().
+__device__ __forceinline__ float fetch_small(const DevTex &t, const AxF &ax, const AxF &ay, const AxF &az) {
+  const uint32_t o = (uint32_t)fmaf(az.fl, t.fpxy4, fmaf(ay.fl, t.fpx4, fmaf(ax.fl, 4.f, t.fbase4)));
   const uint32_t px4 = t.px * 4u, pxy4 = t.pxy * 4u;
   const char *b = reinterpret_cast<const char *>(t.p);
   const f2a4 r00 = *reinterpret_cast<const f2a4 *>(b + o);
@@ -93,6 +121,19 @@ __device__ __forceinline__ float fetch_small(const DevTex &t, const Ax &ax, cons
   const float c01 = lerp(r01.x, r01.y, ax.w), c11 = lerp(r11.x, r11.y, ax.w);
   const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
   return lerp(c0, c1, az.w);
+}
+__device__ __forceinline__ Ax to_ax(const AxF &a) { return Ax{(int)a.fl, a.w}; }
+
+// The LUT value of one light (0 if the illumination texture is unbound).
+__device__ __forceinline__ float lut_light(const DevTex &lut, const AxF &la, float beta, float gamma) {
+  if (lut.p == nullptr) return 0.f;
+  if (lut.one) {
+    const float q = lut.p[0];
+    return fmaf(0.5f, q - q, q);
+  }
+  const AxF lb = axis_f(beta, lut.fny), lg = axis_f(gamma, lut.fnz);
+  if (lut.small) return fetch_small(lut, la, lb, lg);
+  return fetch<false>(lut, to_ax(la), to_ax(lb), to_ax(lg));
 }
 
 // tex3D on any texture state (unbound -> 0, 1x1x1 -> single voxel through the same lerp algebra).
@@ -217,10 +258,45 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
   const float dli = dot3(li, n);
   const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
   const float liplen = sqrt_cr(dot3(lip, lip));
-  const Ax la = axis(alpha_n, P.lut.nx, P.lut.fnx);
-  for (int i = 0; i < P.num_lights; ++i) {
+  const AxF la = axis_f(alpha_n, P.lut.fnx);
+  // lights two at a time: both angle pairs, then both LUT fetches (their loads overlap), then the
+  // accumulation in light order, exactly as the reference's sequential loop
+  int i = 0;
+  for (; i + 1 < P.num_lights; i += 2) {
+    const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+    float beta[2], gamma[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const DevLight &L = j ? L1 : L0;
+      const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);  // lightOut
+#if VR_ABLATE & 2
+      beta[j] = dot3(n, lo) * 0.01f;
+      gamma[j] = dot3(lip, lo) * 0.01f + liplen;
+#else
+      beta[j] = divpi(acosf(div_acos_arg(dot3(n, lo), nlen * sqrt_cr(dot3(lo, lo)))));
+      const float dlo = dot3(lo, n);
+      const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
+      gamma[j] = divpi(acosf(div_acos_arg(dot3(lip, lop), liplen * sqrt_cr(dot3(lop, lop)))));
+#endif
+    }
+#if VR_ABLATE & 1
+    const float light0 = beta[0] + gamma[0] + la.w, light1 = beta[1] + gamma[1] + la.w;
+#else
+    const float light0 = lut_light(P.lut, la, beta[0], gamma[0]);
+    const float light1 = lut_light(P.lut, la, beta[1], gamma[1]);
+#endif
+    const float rl0 = refl * light0;
+    ir = fmaf(rl0 * L0.cr, P.color[0], ir);
+    ig = fmaf(rl0 * L0.cg, P.color[1], ig);
+    ib = fmaf(rl0 * L0.cb, P.color[2], ib);
+    const float rl1 = refl * light1;
+    ir = fmaf(rl1 * L1.cr, P.color[0], ir);
+    ig = fmaf(rl1 * L1.cg, P.color[1], ig);
+    ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+  }
+  if (i < P.num_lights) {
     const DevLight L = P.lights[i];
-    const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);  // lightOut
+    const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
 #if VR_ABLATE & 2
     const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
 #else
@@ -229,20 +305,11 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
     const float gamma = divpi(acosf(div_acos_arg(dot3(lip, lop), liplen * sqrt_cr(dot3(lop, lop)))));
 #endif
-    float light = 0.f;
 #if VR_ABLATE & 1
-    light = beta + gamma + la.w;
-    if (false) {
+    const float light = beta + gamma + la.w;
 #else
-    if (P.lut.p != nullptr) {
+    const float light = lut_light(P.lut, la, beta, gamma);
 #endif
-      if (P.lut.one) {
-        const float q = P.lut.p[0];
-        light = fmaf(0.5f, q - q, q);
-      } else {
-        light = fetch_small(P.lut, la, axis(beta, P.lut.ny, P.lut.fny), axis(gamma, P.lut.nz, P.lut.fnz));
-      }
-    }
     const float rl = refl * light;
     ir = fmaf(rl * L.cr, P.color[0], ir);
     ig = fmaf(rl * L.cg, P.color[1], ig);

@@ -55,26 +55,19 @@ __device__ __forceinline__ float lds_tri(const float *L, const Box &B, int a, fl
 }
 
 // Slot coordinates of a tap pair base and whether the cell [l, l+1] lies in the box along it.
-__device__ __forceinline__ int slot_coord(int i, int r) { return i + 1 - r; }
+__device__ __forceinline__ int slot_coord(int i, int r) { return (int)((uint32_t)i + 1u - (uint32_t)r); }
 __device__ __forceinline__ bool in_box(int l, int e) {
   return (VR_ABLATE & 16) || (unsigned)l < (unsigned)(e - 1);
 }
 
 // Trilinear fetch of the staged emission texture: the slot when the 2x2x2 cell lies in the box
-// (`in`, with slot word `a`), global memory otherwise -- the same interpolation either way.
+// (`in`, with slot word `a`), global memory otherwise -- the same interpolation either way.  The
+// axes are unclamped (axis_raw); the global path clamps them.
 template <bool BIG>
 __device__ __forceinline__ float fetch_at(const DevTex &t, const float *L, const Box &B, bool in, int a,
                                           const Ax &ax, const Ax &ay, const Ax &az) {
   if (in) return lds_tri(L, B, a, ax.w, ay.w, az.w);
-  return fetch<BIG>(t, ax, ay, az);
-}
-
-template <bool BIG>
-__device__ __forceinline__ float fetch_em(const DevTex &t, const float *L, const Box &B, bool staged,
-                                          const Ax &ax, const Ax &ay, const Ax &az) {
-  const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
-  const bool in = staged && in_box(lx, B.ex) && in_box(ly, B.ey) && in_box(lz, B.ez);
-  return fetch_at<BIG>(t, L, B, in, lz * B.pxy + ly * B.px + lx, ax, ay, az);
+  return fetch<BIG>(t, clamp_ax(ax, t.nx), clamp_ax(ay, t.ny), clamp_ax(az, t.nz));
 }
 
 // Padded index range [lo, hi] (inclusive) of the tap pairs of one axis for a coordinate range.
