@@ -162,15 +162,24 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
   return fabsf(v.x) <= 3.4e38f && fabsf(v.y) <= 3.4e38f && fabsf(v.z) <= 3.4e38f;
 }
 
+#ifndef VR_WG_WAVES
+#define VR_WG_WAVES 1  // waves per workgroup (1: a wave's LDS slot is freed as soon as it finishes)
+#endif
+
+// One wave marches one 8x8-pixel tile (lane -> (x = lane >> 3, y = lane & 7)).  Tile t is quadrant
+// (t & 3) of 16x16 block (t >> 2), blocks row-major, t = blockIdx.x * VR_WG_WAVES + wave.  With
+// single-wave workgroups a wave whose rays end early releases its LDS slot at once instead of
+// holding it until the slowest wave of a larger workgroup has finished.
 template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG>
-__global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
-  __shared__ float lds[4][VR_LDS_CAP];
-  int tx, ty;
-  if (!tile_of_block(P, tx, ty)) return;
+__global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderParams P) {
+  __shared__ float lds[VR_WG_WAVES][VR_LDS_CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
-  const int lc = tx * 16 + (wave & 1) * 8 + (lane >> 3);
-  const int y = ty * 16 + (wave >> 1) * 8 + (lane & 7);
+  const int tile = blockIdx.x * VR_WG_WAVES + wave;
+  const int nbx = (P.part_cols + 15) >> 4;
+  const int blk16 = tile >> 2, quad = tile & 3;
+  const int lc = (blk16 % nbx) * 16 + (quad & 1) * 8 + (lane >> 3);
+  const int y = (blk16 / nbx) * 16 + (quad >> 1) * 8 + (lane & 7);
   const bool active = (lc < P.part_cols) && (y < P.height);
   Ray R;
   R.o = mk(0.f, 0.f, 0.f);
@@ -227,11 +236,11 @@ __global__ __launch_bounds__(256) void march_kernel(const RenderParams P) {
 template <int MODE, bool AB, bool SH>
 static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
   if (P.steps) {
-    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, true>), grid, dim3(256), 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, false>), grid, dim3(256), 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, true>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, false>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
   } else {
-    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, true>), grid, dim3(256), 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, false>), grid, dim3(256), 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, true>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, false>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
   }
   return hipGetLastError();
 }
@@ -240,13 +249,8 @@ static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool
 // gradient texture must be the emission texture itself (the reference's tex_emission binding).
 hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s) {
   if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
-  const uint64_t ntx = (P.part_cols + 15) / 16, nty = (P.height + 15) / 16;
-  uint64_t blocks = ntx * nty;
-  if (P.tile_mode == 1) {
-    const uint64_t nsuper = ((ntx + 7) / 8) * ((nty + 7) / 8);
-    blocks = ((nsuper + 7) / 8) * 512;
-  }
-  const dim3 grid((unsigned)blocks);
+  const uint64_t tiles = (uint64_t)((P.part_cols + 15) / 16) * (uint64_t)((P.height + 15) / 16) * 4;
+  const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES));
   switch (mode) {
     case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);
     case 1: return ab_alias ? launch_m<1, true, false>(P, grid, s, big) : launch_m<1, false, false>(P, grid, s, big);
