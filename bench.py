@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--cpu-stride", type=int, default=8, help="CPU baseline: every k-th column")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lights", type=int, default=2, help="light sources (0: emission-absorption only; "
+                    "diagnostics, the metric config has 2)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round1", "traffic.json"),
                     help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
@@ -85,6 +87,7 @@ def main():
     lut = vr.Volume(vr.HenyeyGreenstein(64))
     lut.TimeLastUpdate = np.uint64(7)
     lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+    lights = (lights * ((args.lights + 1) // 2))[: args.lights]
     h = vr.volumeRender("new")
     vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)  # Em, Re, Ab (Ab aliases Em)
     R = rotation(125, 25, 0)
@@ -159,8 +162,8 @@ def main():
         rays = W * H
         ms_per_step = elapsed / args.steps * 1e3
         value = rays * args.steps / elapsed / 1e6
-        L, G = 2, 6
-        F = 1 + (G + 1 + L)  # trilinear fetches per sample, SURVEY.md 8d
+        L, G = args.lights, 6
+        F = 1 + ((G + 1 + L) if L > 0 else 0)  # trilinear fetches per sample, SURVEY.md 8d
         bytes_launch = 4.0 * my_samples * F + 12.0 * my_cols * H
         achieved = bytes_launch / t_kernel_s / 1e9
         result = {
@@ -176,8 +179,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic V_shell(%d) (SURVEY.md 8d), generated in HBM" % n,
-            "config": {"workload": f"V_shell({n}) fp32 {n}^3, {W}x{H}, HG 2 lights (example1.m), on-the-fly "
-                                   "gradient, rotate(125,25,0) f=3 dist=6 thr=0.9",
+            "config": {"workload": f"V_shell({n}) fp32 {n}^3, {W}x{H}, "
+                                   + ("HG 2 lights (example1.m), on-the-fly gradient" if L == 2 else
+                                      f"{L} lights (diagnostic)")
+                                   + ", rotate(125,25,0) f=3 dist=6 thr=0.9",
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": "compute",
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else "")},

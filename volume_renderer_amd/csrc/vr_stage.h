@@ -16,6 +16,9 @@ namespace vr {
 #ifndef VR_LDS_CAP
 #define VR_LDS_CAP 2560  // floats per wave slot (10 KiB; 40 KiB per workgroup -> 4 workgroups per CU)
 #endif
+#ifndef VR_STAGE_UNROLL
+#define VR_STAGE_UNROLL 4  // loads in flight per lane while staging
+#endif
 #ifndef VR_CHUNK
 #define VR_CHUNK 32      // samples per staged chunk (halved while the box does not fit)
 #endif
@@ -23,16 +26,27 @@ namespace vr {
 #define VR_ATTEMPTS 3    // box attempts per chunk: S = VR_CHUNK, /2, /4, ...
 #endif
 
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+// Wave-wide min / max without LDS: DPP row rotations reduce each 16-lane row, then the gfx950
+// permlane16 / permlane32 swaps combine the rows (each returns both halves of the exchange, whose
+// min / max is the xor-16 / xor-32 partner's).  Result made wave-uniform.
+template <bool MAX>
+__device__ __forceinline__ int wave_reduce(int v) {
+  int o = __builtin_amdgcn_update_dpp(v, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v = MAX ? max(v, o) : min(v, o);
+  o = __builtin_amdgcn_update_dpp(v, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v = MAX ? max(v, o) : min(v, o);
+  o = __builtin_amdgcn_update_dpp(v, v, 0x122, 0xf, 0xf, false);  // row_ror:2
+  v = MAX ? max(v, o) : min(v, o);
+  o = __builtin_amdgcn_update_dpp(v, v, 0x121, 0xf, 0xf, false);  // row_ror:1
+  v = MAX ? max(v, o) : min(v, o);
+  const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = MAX ? max((int)p16[0], (int)p16[1]) : min((int)p16[0], (int)p16[1]);
+  const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = MAX ? max((int)p32[0], (int)p32[1]) : min((int)p32[0], (int)p32[1]);
   return __builtin_amdgcn_readfirstlane(v);
 }
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return __builtin_amdgcn_readfirstlane(v);
-}
+__device__ __forceinline__ int wave_min(int v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ int wave_max(int v) { return wave_reduce<true>(v); }
 
 #ifndef VR_ODD_PITCH
 #define VR_ODD_PITCH 0   // 1: odd LDS row / plane pitches (measured slower: larger slots overflow more)
@@ -149,11 +163,11 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
   int l = rr * B.px + xr;  // slot word (pxy == px * ey: row r starts at r * px)
   const int l_row = per * B.px;
   uint32_t acc = 0;
-  for (int k0 = 0; k0 < n; k0 += 4) {
-    float v[4];
-    int li[4];
+  for (int k0 = 0; k0 < n; k0 += VR_STAGE_UNROLL) {
+    float v[VR_STAGE_UNROLL];
+    int li[VR_STAGE_UNROLL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < VR_STAGE_UNROLL; ++j) {
       li[j] = l;
       if (k0 + j < n) v[j] = *reinterpret_cast<const float *>(base + g);
       l += l_row;
@@ -165,7 +179,7 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < VR_STAGE_UNROLL; ++j) {
       if (k0 + j < n) {
         L[li[j]] = v[j];
         acc |= __float_as_uint(v[j]) & 0x7fffffffu;
