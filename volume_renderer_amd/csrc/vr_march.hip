@@ -163,7 +163,7 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 }
 
 #ifndef VR_WG_WAVES
-#define VR_WG_WAVES 1  // waves per workgroup (1: a wave's LDS slot is freed as soon as it finishes)
+#define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif
 
 // One wave marches one 8x8-pixel tile (lane -> (x = lane >> 3, y = lane & 7)).  Tile t is quadrant
