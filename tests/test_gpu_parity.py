@@ -93,6 +93,20 @@ def test_lookup_gradient_then_compute(monkeypatch, counter_clock):
     r.delete()
 
 
+def test_large_illumination_lut(monkeypatch, counter_clock):
+    """A LUT of more than 2^22 padded voxels (168^3) takes the general 64-bit-offset LUT fetch
+    instead of the fp32-offset one; parity against the oracle as for the 64^3 LUT."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(40))
+    r = ex1_renderer(v, res=(64, 48))
+    r.VolumeIllumination = vr.Volume(vr.HenyeyGreenstein(168))
+    img = r.render()
+    assert np.isfinite(img).all() and img.max() > 0
+    print("large LUT parity", tee.renders[-1][2])
+    r.delete()
+
+
 def test_grad_matches_matlab_gradient(counter_clock):
     d = O.rand_volume(12)
     gx, gy, gz = vr.Volume(d).grad()
@@ -286,8 +300,10 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene):
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
-                      ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"})]:
-        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE"):
+                      ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
+                      ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
+                      ("lut_general", {"VR_NO_SMALL_LUT": "1"})]:
+        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT"):
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)

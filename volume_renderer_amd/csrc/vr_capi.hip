@@ -322,6 +322,11 @@ void mm_sync(vr_context *h) {
   }
 }
 
+bool env_flag(const char *name) {
+  const char *ev = std::getenv(name);
+  return ev && ev[0] == '1';
+}
+
 vr::DevTex dev_tex(const BufPtr &b) {
   vr::DevTex t{};
   if (b && b->ptr) {
@@ -336,7 +341,7 @@ vr::DevTex dev_tex(const BufPtr &b) {
     t.fnz = (float)t.nz;
     t.one = (t.nx == 1 && t.ny == 1 && t.nz == 1);
     const uint64_t padded = (b->dims[0] + 2) * (b->dims[1] + 2) * (b->dims[2] + 2);
-    t.small = padded < (1ull << 22);
+    t.small = padded < (1ull << 22) && !env_flag("VR_NO_SMALL_LUT");
     t.fpx4 = 4.f * (float)t.px;
     t.fpxy4 = 4.f * (float)t.pxy;
     t.fbase4 = 4.f * (float)(t.pxy + t.px + 1);
@@ -365,6 +370,7 @@ struct Frame {
   bool ab_alias = false, big = false, share = false;
   bool degenerate = false;
 };
+
 
 int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
   vr::RenderParams &P = F.P;
@@ -474,7 +480,7 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
       if (ev[0] == '1') P.skip_empty = 0;
   }
   F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
-          is_big(P.gz);
+          is_big(P.gz) || env_flag("VR_FORCE_BIG");  // test switch: the 64-bit path on small volumes
   if (is_big(P.lut)) return fail(VR_ERR_UNSUPPORTED, "illumination volume larger than 2^32 voxels");
   bool finite = std::isfinite(P.tstep) && P.tstep > 0.f;
   for (int i = 0; i < 3; ++i) finite = finite && std::isfinite(P.bmin[i]) && std::isfinite(P.bscale[i]);
@@ -526,10 +532,6 @@ int validate_partition(const vr_partition *p) {
   return VR_OK;
 }
 
-bool env_flag(const char *name) {
-  const char *ev = std::getenv(name);
-  return ev && ev[0] == '1';
-}
 
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,

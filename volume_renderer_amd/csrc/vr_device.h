@@ -20,6 +20,7 @@ struct DevTex {
   float fnx, fny, fnz;  // (float)n for the coordinate transform
   int32_t one;    // 1x1x1 volume: every fetch is the single voxel
   int32_t small;  // padded size < 2^22 voxels: byte offsets are exact in fp32 (fetch_small)
+                  // (VR_NO_SMALL_LUT=1 forces the general path, a test switch)
   float fpx4, fpxy4, fbase4;  // 4*px, 4*pxy, 4*(pxy+px+1): byte-offset terms for fetch_small
 };
 
