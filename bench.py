@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--cpu-stride", type=int, default=8, help="CPU baseline: every k-th column")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gradient", choices=["compute", "lookup"], default="compute",
+                    help="lookup: precomputed gradient volumes (example1_grad.m, BASELINE config 3), made on "
+                         "the device with vr_gradient_device")
     ap.add_argument("--lights", type=int, default=2, help="light sources (0: emission-absorption only; "
                     "diagnostics, the metric config has 2)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round1", "traffic.json"),
@@ -89,13 +92,21 @@ def main():
     lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
     lights = (lights * ((args.lights + 1) // 2))[: args.lights]
     h = vr.volumeRender("new")
-    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)  # Em, Re, Ab (Ab aliases Em)
+    grads = []
+    if args.gradient == "lookup":  # Volume.grad on the device, 4 arrays resident
+        grads = [torch.empty_like(vol_t) for _ in range(3)]
+        mex.gradient_device(vol_t.data_ptr(), (n, n, n), *[g.data_ptr() for g in grads], sptr)
+        torch.cuda.synchronize(dev)
+        gvols = [mex.DeviceVolume(g.data_ptr(), (n, n, n), last_update=11 + i, owner=g) for i, g in enumerate(grads)]
+        vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em, *gvols)
+    else:
+        vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)  # Em, Re, Ab (Ab aliases Em)
     R = rotation(125, 25, 0)
     ra, keep = mex.render_args(lights, lut, np.float32([1.0, 0.4, 0.6]), np.float32([1, 1, 1]),
                                np.uint64([H, W]), np.flip(R, 0).astype(np.float32), np.float32([0, 3.0, 6.0]),
                                np.float32(0.9), np.float32([1, 1, 0]))
     host_vol = vol_t.cpu().numpy() if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
-    del vol_t  # the library holds its own resident copy
+    del vol_t, grads  # the library holds its own resident copies
 
     part = mex.partition(args.block_cols, rank, world) if world > 1 else None
     my_cols = mex.partition_columns(W, part)
@@ -162,7 +173,7 @@ def main():
         rays = W * H
         ms_per_step = elapsed / args.steps * 1e3
         value = rays * args.steps / elapsed / 1e6
-        L, G = args.lights, 6
+        L, G = args.lights, (6 if args.gradient == "compute" else 3)
         F = 1 + ((G + 1 + L) if L > 0 else 0)  # trilinear fetches per sample, SURVEY.md 8d
         bytes_launch = 4.0 * my_samples * F + 12.0 * my_cols * H
         achieved = bytes_launch / t_kernel_s / 1e9
@@ -180,10 +191,11 @@ def main():
             "dtype": "f32",
             "data": "synthetic V_shell(%d) (SURVEY.md 8d), generated in HBM" % n,
             "config": {"workload": f"V_shell({n}) fp32 {n}^3, {W}x{H}, "
-                                   + ("HG 2 lights (example1.m), on-the-fly gradient" if L == 2 else
-                                      f"{L} lights (diagnostic)")
+                                   + ("HG 2 lights (example1.m), on-the-fly gradient"
+                                      if (L == 2 and args.gradient == "compute") else
+                                      f"HG {L} lights, {args.gradient} gradient (diagnostic)")
                                    + ", rotate(125,25,0) f=3 dist=6 thr=0.9",
-                       "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": "compute",
+                       "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else "")},
             "samples_per_frame": total_samples,

@@ -141,6 +141,13 @@ int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t b
 /* Synthetic test volume V_shell(n) of SURVEY.md 8d, generated on the device into d_out[n^3]. */
 int vr_synth_shell_device(float *d_out, uint64_t n, void *stream);
 
+/* Volume.grad on the device (Volume.m:181-205, MATLAB gradient() of single data): for the
+ * column-major d_data[d0*d1*d2] writes d_gx (along dim 2), d_gy (along dim 1), d_gz (along dim 3),
+ * central differences inside and one-sided at the ends, bit-identical to MATLAB's single-precision
+ * gradient.  All pointers are device memory; asynchronous on `stream`. */
+int vr_gradient_device(const float *d_data, const uint64_t dims[3], float *d_gx, float *d_gy, float *d_gz,
+                       void *stream);
+
 /* Host-side reproduction of the upload/slot state machine (syncWithDevice,
  * volumeRender_kernel.cu:739-867) for unit tests: returns the slot indices after a sync with the
  * given similarity/update flags starting from `idx` (emission, absorption, reflection). */

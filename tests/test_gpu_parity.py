@@ -107,6 +107,22 @@ def test_large_illumination_lut(monkeypatch, counter_clock):
     r.delete()
 
 
+@pytest.mark.parametrize("shape", [(33, 20, 12), (17, 1, 9), (1, 1, 1), (2, 3, 64)])
+def test_gradient_device_matches_matlab_gradient(shape):
+    """vr_gradient_device (Volume.grad on the GPU) is bit-identical to MATLAB's single gradient."""
+    import torch
+    from volume_renderer_amd import mex
+    rng = np.random.default_rng(7)
+    d = np.asfortranarray(rng.standard_normal(shape).astype(np.float32))
+    t = torch.from_numpy(d.reshape(-1, order="F").copy()).cuda()
+    g = [torch.full_like(t, np.nan) for _ in range(3)]
+    mex.gradient_device(t.data_ptr(), shape, g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr())
+    torch.cuda.synchronize()
+    for got, ref in zip(g, O.matlab_gradient(d)):
+        got = got.cpu().numpy().reshape(shape, order="F")
+        assert np.array_equal(got.view(np.uint32), np.asfortranarray(ref).view(np.uint32))
+
+
 def test_grad_matches_matlab_gradient(counter_clock):
     d = O.rand_volume(12)
     gx, gy, gz = vr.Volume(d).grad()

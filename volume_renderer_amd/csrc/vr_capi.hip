@@ -36,6 +36,7 @@ hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t 
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
 hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s);
+hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, float *gy, float *gz, hipStream_t s);
 }  // namespace vr
 
 namespace {
@@ -764,6 +765,18 @@ int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t b
 int vr_synth_shell_device(float *d_out, uint64_t n, void *stream) {
   VR_GUARD_BEGIN
   VR_HIP(vr::launch_synth_shell(d_out, n, (hipStream_t)stream));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_gradient_device(const float *d_data, const uint64_t dims[3], float *d_gx, float *d_gy, float *d_gz,
+                       void *stream) {
+  if (!dims) return fail(VR_ERR_ARGUMENT, "dims is NULL");
+  if (dims[0] > 0xFFFFFFFFull || dims[1] > 0xFFFFFFFFull || dims[2] > 0xFFFFFFFFull)
+    return fail(VR_ERR_UNSUPPORTED, "dimension above 2^32");
+  if (dims[0] * dims[1] * dims[2] && (!d_data || !d_gx || !d_gy || !d_gz)) return fail(VR_ERR_ARGUMENT, "NULL buffer");
+  VR_GUARD_BEGIN
+  VR_HIP(vr::launch_gradient(d_data, dims, d_gx, d_gy, d_gz, (hipStream_t)stream));
   return VR_OK;
   VR_GUARD_END
 }

@@ -287,6 +287,42 @@ hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc,
   return hipGetLastError();
 }
 
+// MATLAB [gx, gy, gz] = gradient(Data) for single Data(d0, d1, d2) (Volume.m:181-205): gx along
+// dim 2 (d1), gy along dim 1 (d0), gz along dim 3 (d2); (f(i+1) - f(i-1)) / 2 inside, one-sided
+// differences at the ends, 0 along a dimension of extent 1.  fp32 like MATLAB's single gradient:
+// bit-identical to the numpy restatement (oracle.matlab_gradient).  One thread per voxel, x
+// fastest: the three neighbour pairs are coalesced rows / L2-resident planes.
+__device__ __forceinline__ float grad1(const float *p, uint64_t i, uint64_t stride, uint32_t c, uint32_t n) {
+  if (n < 2) return 0.f;
+  if (c == 0) return p[i + stride] - p[i];
+  if (c == n - 1) return p[i] - p[i - stride];
+  return (p[i + stride] - p[i - stride]) / 2.f;
+}
+
+__global__ __launch_bounds__(256) void gradient_kernel(const float *__restrict__ d, uint32_t n0, uint32_t n1,
+                                                       uint32_t n2, float *__restrict__ gx,
+                                                       float *__restrict__ gy, float *__restrict__ gz) {
+  const uint64_t total = (uint64_t)n0 * n1 * n2, plane = (uint64_t)n0 * n1;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < total;
+       q += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = q / plane, r = q - k * plane;
+    const uint32_t j = (uint32_t)(r / n0), i = (uint32_t)(r - (uint64_t)j * n0);
+    gy[q] = grad1(d, q, 1, i, n0);
+    gx[q] = grad1(d, q, n0, j, n1);
+    gz[q] = grad1(d, q, plane, (uint32_t)k, n2);
+  }
+}
+
+hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, float *gy, float *gz, hipStream_t s) {
+  const uint64_t total = dims[0] * dims[1] * dims[2];
+  if (!total) return hipSuccess;
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 262144) blocks = 262144;
+  hipLaunchKernelGGL(gradient_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d, (uint32_t)dims[0],
+                     (uint32_t)dims[1], (uint32_t)dims[2], gx, gy, gz);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s) {
   const uint64_t total = n * n * n;
   if (!total) return hipSuccess;

@@ -194,6 +194,13 @@ def synth_shell_device(d_out: int, n: int, stream: int = 0) -> None:
                                       ctypes.c_void_p(int(stream)) if stream else None))
 
 
+def gradient_device(d_data: int, dims, d_gx: int, d_gy: int, d_gz: int, stream: int = 0) -> None:
+    """Volume.grad on the device (vr_gradient_device): MATLAB gradient() of the column-major single
+    array at d_data with dims (d0, d1, d2) into d_gx (dim 2), d_gy (dim 1), d_gz (dim 3)."""
+    dd = (ctypes.c_uint64 * 3)(*[int(x) for x in dims])
+    _lib.check(_lib.lib().vr_gradient_device(d_data, dd, d_gx, d_gy, d_gz, stream))
+
+
 def volumeRender(cmd, *args):
     """The `volumeRender` mex: commands 'new', 'delete', 'mem_info', 'sync_volumes', 'render'."""
     nrhs = 1 + len(args)
