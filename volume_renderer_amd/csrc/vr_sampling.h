@@ -68,6 +68,29 @@ __device__ __forceinline__ float sqrt_cr(float x) {
   return sqrtf(x);
 }
 
+// sqrt_cr over a group of values with one wave-wide guard (fewer, larger basic blocks for the
+// scheduler): the fast path when every lane's every value qualifies, else the library sqrtf.
+__device__ __forceinline__ float sqrt_fast(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rm = fmaf(-sm, s, x), rp = fmaf(-sp, s, x);
+  const float r = (rm <= 0.f) ? sm : s;
+  return (rp > 0.f) ? sp : r;
+}
+template <int N>
+__device__ __forceinline__ void sqrt_cr_n(const float (&x)[N], float (&out)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < N; ++i) ok = ok && (__float_as_uint(x[i]) - 1u >= 0x0f7fffffu);
+  if (__builtin_expect(__all(ok), 1)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = sqrt_fast(x[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = sqrtf(x[i]);
+  }
+}
+
 __device__ __forceinline__ float lerp(float a, float b, float w) { return fmaf(w, b - a, a); }
 
 // Trilinear fetch from the apron layout given the three axes.
@@ -231,6 +254,28 @@ __device__ __forceinline__ float div_acos_arg(float a, float b) {
   return a / b;
 }
 
+__device__ __forceinline__ float div_fast(float a, float b) {
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float y1 = fmaf(fmaf(-b, y0, 1.f), y0, y0);
+  const float q0 = a * y1;
+  const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
+  return fmaf(fmaf(-b, q1, a), y1, q1);
+}
+// div_acos_arg over a group with one wave-wide guard (see div_acos_arg for the exactness argument).
+template <int N>
+__device__ __forceinline__ void div_acos_n(const float (&a)[N], const float (&b)[N], float (&q)[N]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < N; ++i) ok = ok && ((__float_as_uint(b[i]) & 0x7fffffffu) - 0x2b800000u <= 0x28000000u);
+  if (__builtin_expect(__all(ok), 1)) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = div_fast(a[i], b[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = a[i] / b[i];
+  }
+}
+
 // x / pi, correctly rounded, for x = 0, NaN or x >= 2^-100 -- the range of acosf: x * RN(1/pi)
 // corrected by one fma residual step (3 VALU instead of the 12 of a general IEEE divide).  Equal to
 // the IEEE quotient for every such fp32 x (exhaustive check: tools/microbench/divpi_check.c).
@@ -248,42 +293,56 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
   const float ginv = 1.f / sqrt_cr(dot3(g, g));
   const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
   const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
-  // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle
-  const float nlen = sqrt_cr(dot3(n, n));
-#if VR_ABLATE & 2
-  const float alpha_n = dot3(n, li) * 0.1f;
-#else
-  const float alpha_n = divpi(acosf(div_acos_arg(dot3(n, li), nlen * sqrt_cr(dot3(li, li)))));
-#endif
   const float dli = dot3(li, n);
   const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-  const float liplen = sqrt_cr(dot3(lip, lip));
+  // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle; the
+  // square roots and quotients of one stage share a guard (sqrt_cr_n, div_acos_n)
+  float sq_in[3] = {dot3(n, n), dot3(li, li), dot3(lip, lip)}, sq[3];
+  sqrt_cr_n<3>(sq_in, sq);
+  const float nlen = sq[0], liplen = sq[2];
+  float alpha_n;
+  {
+#if VR_ABLATE & 2
+    alpha_n = dot3(n, li) * 0.1f;
+#else
+    const float num[1] = {dot3(n, li)}, den[1] = {nlen * sq[1]};
+    float q[1];
+    div_acos_n<1>(num, den, q);
+    alpha_n = divpi(acosf(q[0]));
+#endif
+  }
   const AxF la = axis_f(alpha_n, P.lut.fnx);
   // lights two at a time: both angle pairs, then both LUT fetches (their loads overlap), then the
   // accumulation in light order, exactly as the reference's sequential loop
   int i = 0;
   for (; i + 1 < P.num_lights; i += 2) {
     const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
-    float beta[2], gamma[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const DevLight &L = j ? L1 : L0;
-      const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);  // lightOut
+    const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);  // lightOut
+    const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
+    const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
+    const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
+    const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
+    float beta0, gamma0, beta1, gamma1;
 #if VR_ABLATE & 2
-      beta[j] = dot3(n, lo) * 0.01f;
-      gamma[j] = dot3(lip, lo) * 0.01f + liplen;
+    beta0 = dot3(n, lo0) * 0.01f; gamma0 = dot3(lip, lo0) * 0.01f + liplen;
+    beta1 = dot3(n, lo1) * 0.01f; gamma1 = dot3(lip, lo1) * 0.01f + liplen;
 #else
-      beta[j] = divpi(acosf(div_acos_arg(dot3(n, lo), nlen * sqrt_cr(dot3(lo, lo)))));
-      const float dlo = dot3(lo, n);
-      const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-      gamma[j] = divpi(acosf(div_acos_arg(dot3(lip, lop), liplen * sqrt_cr(dot3(lop, lop)))));
+    float li_in[4] = {dot3(lo0, lo0), dot3(lop0, lop0), dot3(lo1, lo1), dot3(lop1, lop1)}, ln[4];
+    sqrt_cr_n<4>(li_in, ln);
+    const float num[4] = {dot3(n, lo0), dot3(lip, lop0), dot3(n, lo1), dot3(lip, lop1)};
+    const float den[4] = {nlen * ln[0], liplen * ln[1], nlen * ln[2], liplen * ln[3]};
+    float q[4];
+    div_acos_n<4>(num, den, q);
+    beta0 = divpi(acosf(q[0]));
+    gamma0 = divpi(acosf(q[1]));
+    beta1 = divpi(acosf(q[2]));
+    gamma1 = divpi(acosf(q[3]));
 #endif
-    }
 #if VR_ABLATE & 1
-    const float light0 = beta[0] + gamma[0] + la.w, light1 = beta[1] + gamma[1] + la.w;
+    const float light0 = beta0 + gamma0 + la.w, light1 = beta1 + gamma1 + la.w;
 #else
-    const float light0 = lut_light(P.lut, la, beta[0], gamma[0]);
-    const float light1 = lut_light(P.lut, la, beta[1], gamma[1]);
+    const float light0 = lut_light(P.lut, la, beta0, gamma0);
+    const float light1 = lut_light(P.lut, la, beta1, gamma1);
 #endif
     const float rl0 = refl * light0;
     ir = fmaf(rl0 * L0.cr, P.color[0], ir);
@@ -297,13 +356,17 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
   if (i < P.num_lights) {
     const DevLight L = P.lights[i];
     const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
+    const float dlo = dot3(lo, n);
+    const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
 #if VR_ABLATE & 2
     const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
 #else
-    const float beta = divpi(acosf(div_acos_arg(dot3(n, lo), nlen * sqrt_cr(dot3(lo, lo)))));
-    const float dlo = dot3(lo, n);
-    const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-    const float gamma = divpi(acosf(div_acos_arg(dot3(lip, lop), liplen * sqrt_cr(dot3(lop, lop)))));
+    float li_in[2] = {dot3(lo, lo), dot3(lop, lop)}, ln[2];
+    sqrt_cr_n<2>(li_in, ln);
+    const float num[2] = {dot3(n, lo), dot3(lip, lop)}, den[2] = {nlen * ln[0], liplen * ln[1]};
+    float q[2];
+    div_acos_n<2>(num, den, q);
+    const float beta = divpi(acosf(q[0])), gamma = divpi(acosf(q[1]));
 #endif
 #if VR_ABLATE & 1
     const float light = beta + gamma + la.w;
