@@ -40,7 +40,7 @@ struct ChunkStats {
 // of the sampler is skipped (the LUT coordinates, which are NaN for a zero gradient, keep it).
 // MODE 0: no lights; 1: on-the-fly gradient from the staged emission texture (gem == em);
 // 2: lookup gradient (gx/gy/gz from global memory, at the centre's axes when SHARE2).
-template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK>
+template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
   const DevTex &E = P.em;
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
@@ -53,7 +53,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     bool staged, partial;
     Box B;
     int box_vol = 0;
-    plan_chunk(P, R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B, COUNT ? &box_vol : nullptr);
+    plan_chunk<CAP>(P, R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B, COUNT ? &box_vol : nullptr);
     if (COUNT && lane == 0) {  // diagnostics: box volume of partial/failed chunks, S of staged ones
       if (!staged || partial) atomicAdd(P.steps + 8 + min(box_vol >> 8, 31), 1ull);
       else atomicAdd(P.steps + 40 + (S >= 32 ? 0 : (S >= 16 ? 1 : (S >= 8 ? 2 : 3))), 1ull);
@@ -170,9 +170,9 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 // (t & 3) of 16x16 block (t >> 2), blocks row-major, t = blockIdx.x * VR_WG_WAVES + wave.  With
 // single-wave workgroups a wave whose rays end early releases its LDS slot at once instead of
 // holding it until the slowest wave of a larger workgroup has finished.
-template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG>
+template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP>
 __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderParams P) {
-  __shared__ float lds[VR_WG_WAVES][VR_LDS_CAP];
+  __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
   const int tile = blockIdx.x * VR_WG_WAVES + wave;
@@ -203,9 +203,9 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderPar
   }
   // every coordinate the march forms from a finite start and step is finite
   if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, false>(P, L, lane, R, C);
+    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
   else
-    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, true>(P, L, lane, R, C);
+    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
   if (active) {
     const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
@@ -233,16 +233,23 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderPar
   }
 }
 
-template <int MODE, bool AB, bool SH>
-static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
+template <int MODE, bool AB, bool SH, int CAP>
+static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
+  const dim3 blk(64 * VR_WG_WAVES);
   if (P.steps) {
-    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, true>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, false>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, true, CAP>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, false, CAP>), grid, blk, 0, s, P);
   } else {
-    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, true>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, false>), grid, dim3(64 * VR_WG_WAVES), 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, true, CAP>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, false, CAP>), grid, blk, 0, s, P);
   }
   return hipGetLastError();
+}
+
+template <int MODE, bool AB, bool SH>
+static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
+  return P.wide_slot ? launch_c<MODE, AB, SH, VR_LDS_CAP_WIDE>(P, grid, s, big)
+                     : launch_c<MODE, AB, SH, VR_LDS_CAP>(P, grid, s, big);
 }
 
 // Host entry: the staged kernel needs a bound, non-constant emission texture; for MODE 1 the

@@ -13,8 +13,13 @@
 
 namespace vr {
 
+// Wave slot sizes (floats).  The march kernel is built for both and the host picks per frame
+// from the camera's texels per pixel (vr_capi.hip): the 8x8-ray footprint grows with it.
 #ifndef VR_LDS_CAP
-#define VR_LDS_CAP 2560  // floats per wave slot (10 KiB; 40 KiB per workgroup -> 4 workgroups per CU)
+#define VR_LDS_CAP 2560        // 10 KiB: 40 KiB per workgroup -> 4 workgroups (16 waves) per CU
+#endif
+#ifndef VR_LDS_CAP_WIDE
+#define VR_LDS_CAP_WIDE 3072   // 12 KiB: 3 workgroups per CU, for footprints above ~1.5 texels/pixel
 #endif
 #ifndef VR_STAGE_UNROLL
 #define VR_STAGE_UNROLL 4  // loads in flight per lane while staging
@@ -199,6 +204,7 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
 // fetch checks every cell against the box), and the chunk may not be leaped.  The predicted end
 // position fma(step, k, pos) is bounded against the k sequentially rounded additions by
 // RenderParams::tap_off.
+template <int CAP>
 __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, const f3 &pos, const f3 &step,
                                            float t, float tfar, int &S, bool &staged, bool &partial, Box &B,
                                            int *vol_out = nullptr) {
@@ -234,7 +240,7 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
     B.pxy = VR_ODD_PITCH ? ((B.px * B.ey) | 1) : B.px * B.ey;
     if (vol_out) *vol_out = B.pxy * B.ez;
     if (B.ex <= 0 || B.ey <= 0 || B.ez <= 0) return;  // no live ray
-    if (B.pxy * B.ez <= VR_LDS_CAP) {
+    if (B.pxy * B.ez <= CAP) {
       staged = true;
       return;
     }
@@ -244,7 +250,7 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
 #if VR_PARTIAL
   // shrink the largest extent about the centre until the sub-box fits (wave-uniform scalars)
   int e[3] = {B.ex, B.ey, B.ez}, r[3] = {B.rx, B.ry, B.rz};
-  while (e[0] * e[1] * e[2] > VR_LDS_CAP) {
+  while (e[0] * e[1] * e[2] > CAP) {
     const int a = (e[0] >= e[1] && e[0] >= e[2]) ? 0 : (e[1] >= e[2] ? 1 : 2);
     if (e[a] <= 2) break;
     r[a] += e[a] & 1;  // trim alternately from the low and the high side
@@ -254,7 +260,7 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
   B.ex = e[0]; B.ey = e[1]; B.ez = e[2];
   B.px = B.ex;
   B.pxy = B.ex * B.ey;
-  if (B.pxy * B.ez <= VR_LDS_CAP) {
+  if (B.pxy * B.ez <= CAP) {
     staged = true;
     partial = true;
     return;
