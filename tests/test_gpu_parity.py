@@ -318,8 +318,8 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene):
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
-                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"})]:
-        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT"):
+                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"}), ("nogvec", {"VR_NO_GVEC": "1"})]:
+        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT", "VR_NO_GVEC"):
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)

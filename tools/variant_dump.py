@@ -15,7 +15,7 @@ from test_gpu_parity import ex1_renderer  # noqa: E402
 VARIANTS = [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
             ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
-                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"})]
+                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"}), ("nogvec", {"VR_NO_GVEC": "1"})]
 out = {}
 for scene in ("hg2", "lookup", "ea"):
     v = vr.Volume(O.shell_volume(56))
@@ -23,11 +23,11 @@ for scene in ("hg2", "lookup", "ea"):
     if scene == "lookup":
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     for name, env in VARIANTS:
-        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT"):
+        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT", "VR_NO_GVEC"):
             os.environ.pop(k, None)
         os.environ.update(env)
         out[f"{scene}_{name}"] = r.render()
-    for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT"):
+    for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT", "VR_NO_GVEC"):
         os.environ.pop(k, None)
     r.delete()
     base = out[f"{scene}_default"]

@@ -53,6 +53,7 @@ struct RenderParams {
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
+  const float *gvec;              // lookup gradient interleaved (gx,gy,gz,0) x padded voxels, or null
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)

@@ -323,6 +323,22 @@ hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, fl
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void interleave3_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                          const float *__restrict__ c, float4 *__restrict__ out,
+                                                          uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = make_float4(a[i], b[i], c[i], 0.f);
+}
+
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 262144) blocks = 262144;
+  hipLaunchKernelGGL(interleave3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
+                     reinterpret_cast<float4 *>(out), n);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s) {
   const uint64_t total = n * n * n;
   if (!total) return hipSuccess;

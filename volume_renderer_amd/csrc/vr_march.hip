@@ -129,7 +129,10 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
         } else if (SHARE2) {
           const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
-          g = mk(fetch<BIG>(P.gx, cx, cy, cz), fetch<BIG>(P.gy, cx, cy, cz), fetch<BIG>(P.gz, cx, cy, cz));
+          if (P.gvec)
+            g = fetch_vec<BIG>(P.gvec, P.gx, cx, cy, cz);
+          else
+            g = mk(fetch<BIG>(P.gx, cx, cy, cz), fetch<BIG>(P.gy, cx, cy, cz), fetch<BIG>(P.gz, cx, cy, cz));
         } else {
           g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
                  tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));

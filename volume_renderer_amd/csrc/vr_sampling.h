@@ -159,6 +159,32 @@ __device__ __forceinline__ float lut_light(const DevTex &lut, const AxF &la, flo
   return fetch<false>(lut, to_ax(la), to_ax(lb), to_ax(lg));
 }
 
+// Trilinear fetch of the three lookup-gradient textures at once from their interleaved copy
+// (RenderParams::gvec, pitches of `t`): per row the x-pair is two aligned 16-byte loads, and each
+// component goes through exactly the interpolation fetch() applies to its own texture.
+template <bool BIG>
+__device__ __forceinline__ f3 fetch_vec(const float *gvec, const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
+  uint64_t o;
+  if (BIG) o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
+  else o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
+  const float4 *b = reinterpret_cast<const float4 *>(gvec) + o;
+  const float4 a00 = b[0], b00 = b[1], a10 = b[t.px], b10 = b[t.px + 1];
+  const float4 a01 = b[t.pxy], b01 = b[t.pxy + 1], a11 = b[t.pxy + t.px], b11 = b[t.pxy + t.px + 1];
+  f3 r;
+#define VR_TRI(c)                                                                                  \
+  {                                                                                                \
+    const float c00 = lerp(a00.c, b00.c, ax.w), c10 = lerp(a10.c, b10.c, ax.w);                    \
+    const float c01 = lerp(a01.c, b01.c, ax.w), c11 = lerp(a11.c, b11.c, ax.w);                    \
+    const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);                              \
+    r.c = lerp(c0, c1, az.w);                                                                      \
+  }
+  VR_TRI(x)
+  VR_TRI(y)
+  VR_TRI(z)
+#undef VR_TRI
+  return r;
+}
+
 // tex3D on any texture state (unbound -> 0, 1x1x1 -> single voxel through the same lerp algebra).
 template <bool BIG>
 __device__ __forceinline__ float tex3d(const DevTex &t, float x, float y, float z) {
