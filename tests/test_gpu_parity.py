@@ -191,12 +191,44 @@ def test_slot_stickiness(monkeypatch, counter_clock):
     r.render()
     r.VolumeEmission = vr.Volume(O.shell_volume(32) * np.float32(0.7))
     r.render()
-    # Emission == Absorption with only Reflection re-stamped: the simEmAb typo path
-    # (kernel.cu:853-856) routes emission through the reflection texture.
+    # a new Reflection volume: every slot index still names the emission texture
     r.VolumeReflection = vr.Volume(O.rand_volume(16))
     r.render()
     assert len(tee.renders) == 3
     r.delete()
+
+
+@pytest.mark.parametrize("zero_front", [False, True])
+def test_emission_through_reflection_slot(monkeypatch, counter_clock, zero_front):
+    """Emission == Absorption with only Reflection re-stamped takes the simEmAb branch of the
+    volume sync (volumeRender_kernel.cu:853-856): d_idxEmmission becomes the reflection texture
+    and the emission texture is unbound.  A second handle then binds its own emission texture
+    (module-global), so its render samples emission from ITS reflection volume and absorption
+    (d_idxAbsorption = emission) from its emission volume: two distinct bound textures.  Without
+    lights the staged march runs; the reflection volume is zero on half of the box where the
+    absorption is not, so the march must not leap chunks that are empty in the emission texture
+    alone (the opacity accumulated there dims what lies behind)."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(32))
+    r1 = ex1_renderer(v, res=(64, 48), lights=False)
+    r1.VolumeAbsorption = v
+    r1.VolumeReflection = vr.Volume(O.rand_volume(16))
+    r1.render()
+    r1.VolumeReflection = vr.Volume(O.rand_volume(16))
+    r1.render()
+    half = O.shell_volume(40).copy(order="F")
+    if zero_front:
+        half[:, :, :20] = 0
+    else:
+        half[:, :, 20:] = 0
+    r2 = ex1_renderer(vr.Volume(O.shell_volume(40)), res=(64, 48), lights=False)
+    r2.VolumeAbsorption = vr.Volume(O.rand_volume(12))
+    r2.VolumeReflection = vr.Volume(half)
+    img = r2.render()
+    assert img.any() and len(tee.renders) == 3
+    r2.delete()
+    r1.delete()
 
 
 def test_two_handles_share_module_state(monkeypatch, counter_clock):

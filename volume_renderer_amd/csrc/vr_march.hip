@@ -61,7 +61,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     bool empty = false;
     if (staged) {
       const bool nonzero = stage_box<BIG>(L, E, B, lane);  // always stage: the samples read the slot
-      empty = P.skip_empty && !partial && !nonzero;
+      // leap only when the absorption texture is the staged one: a zero emission box says nothing
+      // about the opacity of a separate absorption texture (the simEmAb slot path)
+      empty = AB_ALIAS && P.skip_empty && !partial && !nonzero;
     }
     __builtin_amdgcn_wave_barrier();
     if (COUNT) ++(staged && !partial ? (empty ? C.leap : C.staged) : C.fall);
