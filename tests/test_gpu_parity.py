@@ -337,11 +337,16 @@ def test_step_count_matches_oracle(counter_clock):
     r.delete()
 
 
+@pytest.mark.parametrize("shade", ["fast", "exact"])
 @pytest.mark.parametrize("scene", ["hg2", "lookup", "ea"])
-def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene):
+def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, shade):
     """The LDS-staged march, the plain kernel, the empty-sample skip / empty-chunk leap and the
     XCD tile order change only where data comes from and which exact no-ops are elided: the
-    images must agree bit for bit."""
+    images must agree bit for bit, with either shading arithmetic."""
+    if shade == "exact":
+        monkeypatch.setenv("VR_EXACT_SHADE", "1")
+    else:
+        monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
     v = vr.Volume(O.shell_volume(56))
     r = ex1_renderer(v, res=(120, 88), lights=(scene != "ea"))
     if scene == "lookup":
@@ -360,4 +365,26 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene):
     assert base.max() > 0
     for name, img in imgs.items():
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
+    r.delete()
+
+
+@pytest.mark.parametrize("scene", ["hg2", "lookup"])
+def test_exact_shading_matches_oracle(monkeypatch, counter_clock, scene):
+    """VR_EXACT_SHADE=1: the oracle's op sequence (correctly rounded roots and quotients, expf);
+    only acosf comes from a different library, so most pixel-channels are bit-identical and the
+    rest within the tolerance.  The default (fast) shading must also be within the tolerance of
+    the same oracle render and close to the exact one."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(48))
+    r = ex1_renderer(v, res=(96, 72))
+    if scene == "lookup":
+        r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
+    monkeypatch.setenv("VR_EXACT_SHADE", "1")
+    exact = r.render()
+    monkeypatch.delenv("VR_EXACT_SHADE")
+    fast = r.render()
+    assert len(tee.renders) == 2
+    assert tee.renders[0][2]["bit_exact"] > 0.5, tee.renders[0][2]
+    assert np.abs(fast - exact).max() <= 1e-2 * exact.max()
     r.delete()

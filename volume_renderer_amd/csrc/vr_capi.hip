@@ -30,7 +30,12 @@
 
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
+namespace fast {  // vr_march.hip built with VR_MARCH_FAST=1 / 0
 hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s);
+}
+namespace exact {
+hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s);
+}
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
@@ -584,6 +589,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     P.wide_slot = tau > 1.5 ? 1 : 0;
     if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
   }
+  // shading arithmetic: hardware rsq / exp2 by default; VR_EXACT_SHADE=1 selects
+  // the oracle's correctly rounded op sequence (bit-identical to oracle/vr_oracle.c up to acosf)
+  P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
   if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
   if (F.degenerate) {
@@ -623,7 +631,10 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     if (g_tex.gvec) P.gvec = g_tex.gvec->ptr;
   }
   if (march) {
-    VR_HIP(vr::launch_march(P, F.mode, F.ab_alias, F.share, F.big, stream));
+    if (P.fast_shade)
+      VR_HIP(vr::fast::launch_march(P, F.mode, F.ab_alias, F.share, F.big, stream));
+    else
+      VR_HIP(vr::exact::launch_march(P, F.mode, F.ab_alias, F.share, F.big, stream));
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
   }

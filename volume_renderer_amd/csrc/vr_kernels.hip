@@ -9,8 +9,9 @@
 // Numerics: the ray set-up, the march recurrences (t += tstep, pos += step), the
 // sample coordinates, the 8-bit filter weights and the lerps follow the oracle op for op (explicit
 // fmaf, -ffp-contract=off), so sample positions and texel fetches are bit-identical to the oracle.
-// Shading (normalize, lengths, angles) is the oracle's op sequence with correctly rounded
-// sqrt/div; only expf/acosf come from the device math library (<= 1 ulp from glibc).
+// Shading: FAST (the default) forms the angle cosines with the hardware reciprocal square root and
+// __expf as exp2 (vr_sampling.h shade_lights / opacity); FAST = false is the oracle's op sequence
+// with correctly rounded sqrt/div, only expf/acosf from the device math library.
 //
 // Memory: volumes live in the apron layout of vr_device.h, so every trilinear fetch
 // is 4 x global_load_dwordx2 (one per (y,z) row of the 2x2x2 cell) with no per-tap clamping; the
@@ -30,7 +31,7 @@ namespace vr {
 // MODE 0: no light sources (shade() contributes exactly 0); 1: on-the-fly gradient; 2: lookup.
 // SHARE: the gradient texture(s) have the emission texture's dims, so the unshifted axes of the
 // gradient taps (MODE 1) / all axes of the lookups (MODE 2) are the centre sample's.
-template <int MODE, bool AB_ALIAS, bool BIG, bool COUNT, bool SHARE>
+template <int MODE, bool AB_ALIAS, bool BIG, bool COUNT, bool SHARE, bool FAST>
 __global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderParams P) {
   // 16x16 pixel workgroup tile; wave w owns the 8x8 quadrant (w & 1, w >> 1); lane -> (x, y)
   // with y fastest so that the column-major output stores of a lane octet are contiguous.
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderP
         const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
         const float e = P.fe * em_s;
         const float a = P.fa * ab_s;
-        const float alpha = 1.f - expf(-a * tstep);
+        const float alpha = opacity<FAST>(a, tstep);
         const float eds = e * tstep;
         float ir = 0.f, ig = 0.f, ib = 0.f;
         // opacity exactly 0 and a finite emission term: the sample adds exactly 0 (every other
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderP
                      tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
           }
           const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
-          shade_lights(P, g, pos, o, refl, ir, ig, ib);
+          shade_lights<FAST>(P, g, pos, o, refl, ir, ig, ib);
         }
         const float r = fmaf(eds, P.color[0], ir) * alpha;
         const float gg = fmaf(eds, P.color[1], ig) * alpha;
@@ -242,10 +243,17 @@ __global__ __launch_bounds__(256) void stats_kernel(const float *__restrict__ sr
 
 template <int MODE, bool AB, bool BIG, bool SH>
 static hipError_t launch4(const RenderParams &P, dim3 grid, hipStream_t s) {
-  if (P.steps)
-    hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, true, SH>), grid, dim3(256), 0, s, P);
-  else
-    hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, false, SH>), grid, dim3(256), 0, s, P);
+  if (P.fast_shade) {
+    if (P.steps)
+      hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, true, SH, true>), grid, dim3(256), 0, s, P);
+    else
+      hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, false, SH, true>), grid, dim3(256), 0, s, P);
+  } else {
+    if (P.steps)
+      hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, true, SH, false>), grid, dim3(256), 0, s, P);
+    else
+      hipLaunchKernelGGL((render_kernel<MODE, AB, BIG, false, SH, false>), grid, dim3(256), 0, s, P);
+  }
   return hipGetLastError();
 }
 

@@ -22,6 +22,17 @@
 
 namespace vr {
 
+// Built twice (Makefile): VR_MARCH_FAST=1 -> vr::fast (the default shading),
+// VR_MARCH_FAST=0 -> vr::exact (op for op the oracle's).  Everything else is shared.
+#ifndef VR_MARCH_FAST
+#define VR_MARCH_FAST 1
+#endif
+#if VR_MARCH_FAST
+namespace fast {
+#else
+namespace exact {
+#endif
+
 // Per-lane march state carried across chunks.
 struct Ray {
   f3 o, pos, step;
@@ -89,11 +100,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
       const float e = P.fe * em_s;
       const float a = P.fa * ab_s;
-#if VR_ABLATE & 8
-      const float alpha = a * tstep;
-#else
-      const float alpha = 1.f - expf(-a * tstep);
-#endif
+      const float alpha = opacity<VR_MARCH_FAST>(a, tstep);
       const float eds = e * tstep;
       float ir = 0.f, ig = 0.f, ib = 0.f;
       const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
@@ -140,7 +147,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
                  tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
         }
         const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
-        shade_lights(P, g, pos, R.o, refl, ir, ig, ib);
+        shade_lights<VR_MARCH_FAST>(P, g, pos, R.o, refl, ir, ig, ib);
       }
       const float r = fmaf(eds, P.color[0], ir) * alpha;
       const float gg = fmaf(eds, P.color[1], ig) * alpha;
@@ -272,4 +279,5 @@ hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool sha
   }
 }
 
+}  // namespace fast / exact
 }  // namespace vr

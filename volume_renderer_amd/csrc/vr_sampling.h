@@ -311,98 +311,168 @@ __device__ __forceinline__ float divpi(float x) {
   return fmaf(fmaf(-q, VR_PI, x), r, q);
 }
 
+// acos(q) / pi in one rounding (device library acospi) for the fast shading variant
+extern "C" __device__ float __ocml_acospi_f32(float);
+__device__ __forceinline__ float acospi_q(float q) { return __ocml_acospi_f32(q); }
+
+// 1 - __expf(-a * dx) (volumeRender_kernel.cu:456).  Exact variant: the correctly rounded-ish
+// device expf the oracle models; fast variant: what __expf is, exp2 of x * log2(e) on the
+// hardware exp unit (v_exp_f32).
+template <bool FAST>
+__device__ __forceinline__ float opacity(float a, float tstep) {
+#if VR_ABLATE & 8
+  return a * tstep;
+#else
+  if constexpr (FAST) return 1.f - __builtin_amdgcn_exp2f((-a * tstep) * 0x1.715476p+0f);
+  else return 1.f - expf(-a * tstep);
+#endif
+}
+
+// FAST = false: op for op the oracle's shading (correctly rounded roots and quotients; only acosf
+// comes from the device library).  FAST = true (the default): the angle cosines as
+// dot(a,b) * rsq(a.a) * rsq(b.b) with the hardware reciprocal square root (1 ulp, as the
+// reference's own rsqrtf normalize) and acos/pi in one step; within the parity tolerance of
+// SURVEY.md 8c, about 10 % faster at the metric configuration.
+template <bool FAST>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib) {
-  // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
-  // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n below
-  // cancel when the view ray is parallel to n, and gamma then depends on every bit of n.
-  const float ginv = 1.f / sqrt_cr(dot3(g, g));
-  const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
-  const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
-  const float dli = dot3(li, n);
-  const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-  // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle; the
-  // square roots and quotients of one stage share a guard (sqrt_cr_n, div_acos_n)
-  float sq_in[3] = {dot3(n, n), dot3(li, li), dot3(lip, lip)}, sq[3];
-  sqrt_cr_n<3>(sq_in, sq);
-  const float nlen = sq[0], liplen = sq[2];
-  float alpha_n;
-  {
+  if constexpr (FAST) {
+    // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
+    const float ginv = __builtin_amdgcn_rsqf(dot3(g, g));
+    const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
+    const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
+    const float dli = dot3(li, n);
+    const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
+    const float rn = __builtin_amdgcn_rsqf(dot3(n, n)), rlip = __builtin_amdgcn_rsqf(dot3(lip, lip));
+    const float alpha_n = acospi_q(dot3(n, li) * (rn * __builtin_amdgcn_rsqf(dot3(li, li))));
+    const AxF la = axis_f(alpha_n, P.lut.fnx);
+    int i = 0;
+    for (; i + 1 < P.num_lights; i += 2) {
+      const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+      const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
+      const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
+      const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
+      const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
+      const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
+      const float beta0 = acospi_q(dlo0 * (rn * __builtin_amdgcn_rsqf(dot3(lo0, lo0))));
+      const float gamma0 = acospi_q(dot3(lip, lop0) * (rlip * __builtin_amdgcn_rsqf(dot3(lop0, lop0))));
+      const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
+      const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
+      const float light0 = lut_light(P.lut, la, beta0, gamma0);
+      const float light1 = lut_light(P.lut, la, beta1, gamma1);
+      const float rl0 = refl * light0;
+      ir = fmaf(rl0 * L0.cr, P.color[0], ir);
+      ig = fmaf(rl0 * L0.cg, P.color[1], ig);
+      ib = fmaf(rl0 * L0.cb, P.color[2], ib);
+      const float rl1 = refl * light1;
+      ir = fmaf(rl1 * L1.cr, P.color[0], ir);
+      ig = fmaf(rl1 * L1.cg, P.color[1], ig);
+      ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+    }
+    if (i < P.num_lights) {
+      const DevLight L = P.lights[i];
+      const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
+      const float dlo = dot3(lo, n);
+      const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
+      const float beta = acospi_q(dlo * (rn * __builtin_amdgcn_rsqf(dot3(lo, lo))));
+      const float gamma = acospi_q(dot3(lip, lop) * (rlip * __builtin_amdgcn_rsqf(dot3(lop, lop))));
+      const float rl = refl * lut_light(P.lut, la, beta, gamma);
+      ir = fmaf(rl * L.cr, P.color[0], ir);
+      ig = fmaf(rl * L.cg, P.color[1], ig);
+      ib = fmaf(rl * L.cb, P.color[2], ib);
+    }
+  } else {
+    // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
+    // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n below
+    // cancel when the view ray is parallel to n, and gamma then depends on every bit of n.
+    const float ginv = 1.f / sqrt_cr(dot3(g, g));
+    const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
+    const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);  // lightIn = eye - pos
+    const float dli = dot3(li, n);
+    const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
+    // angle(a,b)/pi = acos(dot(a,b) / (length(a)*length(b))) / PI, op for op as the oracle; the
+    // square roots and quotients of one stage share a guard (sqrt_cr_n, div_acos_n)
+    float sq_in[3] = {dot3(n, n), dot3(li, li), dot3(lip, lip)}, sq[3];
+    sqrt_cr_n<3>(sq_in, sq);
+    const float nlen = sq[0], liplen = sq[2];
+    float alpha_n;
+    {
 #if VR_ABLATE & 2
-    alpha_n = dot3(n, li) * 0.1f;
+      alpha_n = dot3(n, li) * 0.1f;
 #else
-    const float num[1] = {dot3(n, li)}, den[1] = {nlen * sq[1]};
-    float q[1];
-    div_acos_n<1>(num, den, q);
-    alpha_n = divpi(acosf(q[0]));
+      const float num[1] = {dot3(n, li)}, den[1] = {nlen * sq[1]};
+      float q[1];
+      div_acos_n<1>(num, den, q);
+      alpha_n = divpi(acosf(q[0]));
 #endif
-  }
-  const AxF la = axis_f(alpha_n, P.lut.fnx);
-  // lights two at a time: both angle pairs, then both LUT fetches (their loads overlap), then the
-  // accumulation in light order, exactly as the reference's sequential loop
-  int i = 0;
-  for (; i + 1 < P.num_lights; i += 2) {
-    const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
-    const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);  // lightOut
-    const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
-    const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
-    const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
-    const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-    float beta0, gamma0, beta1, gamma1;
+    }
+    const AxF la = axis_f(alpha_n, P.lut.fnx);
+    // lights two at a time: both angle pairs, then both LUT fetches (their loads overlap), then the
+    // accumulation in light order, exactly as the reference's sequential loop
+    int i = 0;
+    for (; i + 1 < P.num_lights; i += 2) {
+      const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+      const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);  // lightOut
+      const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
+      const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
+      const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
+      const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
+      float beta0, gamma0, beta1, gamma1;
 #if VR_ABLATE & 2
-    beta0 = dot3(n, lo0) * 0.01f; gamma0 = dot3(lip, lo0) * 0.01f + liplen;
-    beta1 = dot3(n, lo1) * 0.01f; gamma1 = dot3(lip, lo1) * 0.01f + liplen;
+      beta0 = dot3(n, lo0) * 0.01f; gamma0 = dot3(lip, lo0) * 0.01f + liplen;
+      beta1 = dot3(n, lo1) * 0.01f; gamma1 = dot3(lip, lo1) * 0.01f + liplen;
 #else
-    float li_in[4] = {dot3(lo0, lo0), dot3(lop0, lop0), dot3(lo1, lo1), dot3(lop1, lop1)}, ln[4];
-    sqrt_cr_n<4>(li_in, ln);
-    const float num[4] = {dot3(n, lo0), dot3(lip, lop0), dot3(n, lo1), dot3(lip, lop1)};
-    const float den[4] = {nlen * ln[0], liplen * ln[1], nlen * ln[2], liplen * ln[3]};
-    float q[4];
-    div_acos_n<4>(num, den, q);
-    beta0 = divpi(acosf(q[0]));
-    gamma0 = divpi(acosf(q[1]));
-    beta1 = divpi(acosf(q[2]));
-    gamma1 = divpi(acosf(q[3]));
+      float li_in[4] = {dot3(lo0, lo0), dot3(lop0, lop0), dot3(lo1, lo1), dot3(lop1, lop1)}, ln[4];
+      sqrt_cr_n<4>(li_in, ln);
+      const float num[4] = {dot3(n, lo0), dot3(lip, lop0), dot3(n, lo1), dot3(lip, lop1)};
+      const float den[4] = {nlen * ln[0], liplen * ln[1], nlen * ln[2], liplen * ln[3]};
+      float q[4];
+      div_acos_n<4>(num, den, q);
+      beta0 = divpi(acosf(q[0]));
+      gamma0 = divpi(acosf(q[1]));
+      beta1 = divpi(acosf(q[2]));
+      gamma1 = divpi(acosf(q[3]));
 #endif
 #if VR_ABLATE & 1
-    const float light0 = beta0 + gamma0 + la.w, light1 = beta1 + gamma1 + la.w;
+      const float light0 = beta0 + gamma0 + la.w, light1 = beta1 + gamma1 + la.w;
 #else
-    const float light0 = lut_light(P.lut, la, beta0, gamma0);
-    const float light1 = lut_light(P.lut, la, beta1, gamma1);
+      const float light0 = lut_light(P.lut, la, beta0, gamma0);
+      const float light1 = lut_light(P.lut, la, beta1, gamma1);
 #endif
-    const float rl0 = refl * light0;
-    ir = fmaf(rl0 * L0.cr, P.color[0], ir);
-    ig = fmaf(rl0 * L0.cg, P.color[1], ig);
-    ib = fmaf(rl0 * L0.cb, P.color[2], ib);
-    const float rl1 = refl * light1;
-    ir = fmaf(rl1 * L1.cr, P.color[0], ir);
-    ig = fmaf(rl1 * L1.cg, P.color[1], ig);
-    ib = fmaf(rl1 * L1.cb, P.color[2], ib);
-  }
-  if (i < P.num_lights) {
-    const DevLight L = P.lights[i];
-    const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
-    const float dlo = dot3(lo, n);
-    const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
+      const float rl0 = refl * light0;
+      ir = fmaf(rl0 * L0.cr, P.color[0], ir);
+      ig = fmaf(rl0 * L0.cg, P.color[1], ig);
+      ib = fmaf(rl0 * L0.cb, P.color[2], ib);
+      const float rl1 = refl * light1;
+      ir = fmaf(rl1 * L1.cr, P.color[0], ir);
+      ig = fmaf(rl1 * L1.cg, P.color[1], ig);
+      ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+    }
+    if (i < P.num_lights) {
+      const DevLight L = P.lights[i];
+      const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
+      const float dlo = dot3(lo, n);
+      const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
 #if VR_ABLATE & 2
-    const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
+      const float beta = dot3(n, lo) * 0.01f, gamma = dot3(lip, lo) * 0.01f + liplen;
 #else
-    float li_in[2] = {dot3(lo, lo), dot3(lop, lop)}, ln[2];
-    sqrt_cr_n<2>(li_in, ln);
-    const float num[2] = {dot3(n, lo), dot3(lip, lop)}, den[2] = {nlen * ln[0], liplen * ln[1]};
-    float q[2];
-    div_acos_n<2>(num, den, q);
-    const float beta = divpi(acosf(q[0])), gamma = divpi(acosf(q[1]));
+      float li_in[2] = {dot3(lo, lo), dot3(lop, lop)}, ln[2];
+      sqrt_cr_n<2>(li_in, ln);
+      const float num[2] = {dot3(n, lo), dot3(lip, lop)}, den[2] = {nlen * ln[0], liplen * ln[1]};
+      float q[2];
+      div_acos_n<2>(num, den, q);
+      const float beta = divpi(acosf(q[0])), gamma = divpi(acosf(q[1]));
 #endif
 #if VR_ABLATE & 1
-    const float light = beta + gamma + la.w;
+      const float light = beta + gamma + la.w;
 #else
-    const float light = lut_light(P.lut, la, beta, gamma);
+      const float light = lut_light(P.lut, la, beta, gamma);
 #endif
-    const float rl = refl * light;
-    ir = fmaf(rl * L.cr, P.color[0], ir);
-    ig = fmaf(rl * L.cg, P.color[1], ig);
-    ib = fmaf(rl * L.cb, P.color[2], ib);
+      const float rl = refl * light;
+      ir = fmaf(rl * L.cr, P.color[0], ir);
+      ig = fmaf(rl * L.cg, P.color[1], ig);
+      ib = fmaf(rl * L.cb, P.color[2], ib);
+    }
   }
 }
 
