@@ -58,6 +58,9 @@ def main():
                          "the device with vr_gradient_device")
     ap.add_argument("--lights", type=int, default=2, help="light sources (0: emission-absorption only; "
                     "diagnostics, the metric config has 2)")
+    ap.add_argument("--sim-parts", type=int, default=0,
+                    help="diagnostic (1 GPU): also time each rank's share of a P-way column partition, "
+                         "the kernel time a rank would see at --gpus P")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round1", "traffic.json"),
                     help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
@@ -159,6 +162,24 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
 
+    sim = None
+    if args.sim_parts > 1 and world == 1:
+        P_ = args.sim_parts
+        pcols = max(mex.partition_columns(W, mex.partition(args.block_cols, p, P_)) for p in range(P_))
+        sim_out = torch.zeros(3 * pcols * H, dtype=torch.float32, device=dev)
+        sim = []
+        for p in range(P_):
+            pp = mex.partition(args.block_cols, p, P_)
+            mex.render_device(h, ra, sim_out.data_ptr(), pp, 0, sptr)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(3):
+                mex.render_device(h, ra, sim_out.data_ptr(), pp, 0, sptr)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            sim.append(round(e0.elapsed_time(e1) / 3, 3))
+        del sim_out
+
     samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -212,6 +233,9 @@ def main():
                          "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F},
             "cpu_baseline": None,
         }
+        if sim is not None:
+            result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
+                                             "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
 
     # ---- CPU baseline: the oracle (C, OpenMP) on every k-th column of the same frame -----------
     if rank == 0 and world == 1 and host_vol is not None:

@@ -341,22 +341,30 @@ def test_step_count_matches_oracle(counter_clock):
 @pytest.mark.parametrize("scene", ["hg2", "lookup", "ea"])
 def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, shade):
     """The LDS-staged march, the plain kernel, the empty-sample skip / empty-chunk leap and the
-    XCD tile order change only where data comes from and which exact no-ops are elided: the
-    images must agree bit for bit, with either shading arithmetic."""
+    XCD tile order and the depth lanes (K lanes per ray compositing K consecutive samples) change
+    only where data comes from, which exact no-ops are elided and which lane computes a sample:
+    the images must agree bit for bit, with either shading arithmetic.  The image
+    size is ragged for every tile shape."""
     if shade == "exact":
         monkeypatch.setenv("VR_EXACT_SHADE", "1")
     else:
         monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
     v = vr.Volume(O.shell_volume(56))
-    r = ex1_renderer(v, res=(120, 88), lights=(scene != "ea"))
+    r = ex1_renderer(v, res=(121, 87), lights=(scene != "ea"))
     if scene == "lookup":
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
+    keys = ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT",
+            "VR_NO_GVEC", "VR_DEPTH_LANES")
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
-                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"}), ("nogvec", {"VR_NO_GVEC": "1"})]:
-        for k in ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT", "VR_NO_GVEC"):
+                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"}), ("nogvec", {"VR_NO_GVEC": "1"}),
+                      ("k1", {"VR_DEPTH_LANES": "1"}), ("k2", {"VR_DEPTH_LANES": "2"}), ("k4", {"VR_DEPTH_LANES": "4"}),
+                      ("k8", {"VR_DEPTH_LANES": "8"}), ("k2_noskip", {"VR_DEPTH_LANES": "2", "VR_NO_EMPTY_SKIP": "1"}),
+                      ("k8_wide", {"VR_DEPTH_LANES": "8", "VR_WIDE_SLOT": "1"}),
+                      ("k4_big", {"VR_DEPTH_LANES": "4", "VR_FORCE_BIG": "1"})]:
+        for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)

@@ -30,12 +30,17 @@
 
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
-namespace fast {  // vr_march.hip built with VR_MARCH_FAST=1 / 0
-hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s);
-}
-namespace exact {
-hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s);
-}
+// vr_march.hip built with VR_MARCH_FAST=1 / 0 (namespaces fast / exact) and VR_MARCH_K = 1, 2, 4, 8
+#define VR_DECL_MARCH(ns)                                                                                 \
+  namespace ns {                                                                                         \
+  hipError_t launch_march_k1(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
+  hipError_t launch_march_k2(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
+  hipError_t launch_march_k4(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
+  hipError_t launch_march_k8(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
+  }
+VR_DECL_MARCH(fast)
+VR_DECL_MARCH(exact)
+#undef VR_DECL_MARCH
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
@@ -44,6 +49,13 @@ hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc,
 hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s);
 hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, float *gy, float *gz, hipStream_t s);
 }  // namespace vr
+
+#ifndef VR_DEPTH_ROUNDS_K1
+#define VR_DEPTH_ROUNDS_K1 16.0  // K = 1 at >= this many K = 1 waves per device wave slot (tuned on MI355X)
+#endif
+#ifndef VR_DEPTH_ROUNDS_K2
+#define VR_DEPTH_ROUNDS_K2 3.0   // K = 2 at >= this many, K = 4 below
+#endif
 
 namespace {
 
@@ -550,6 +562,35 @@ int validate_partition(const vr_partition *p) {
 }
 
 
+// Depth lanes of the march kernel (lanes per ray).  One wave marches 64 / K rays;
+// its run time is that of its longest ray, so the launch lasts at least as long as the slowest
+// wave however many the GPU runs at once.  With few waves per wave slot of the device (a small
+// image, or one GPU's share of a multi-GPU partition) K > 1 cuts that tail K-fold; with many,
+// K = 1 avoids the per-group compositing overhead.  VR_DEPTH_LANES=1/2/4/8 overrides.
+int device_wave_slots() {
+  static int slots = 0;
+  if (!slots) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    }
+    slots = cus * 16;  // 4 workgroups of 4 waves per CU (10 KiB LDS slots)
+  }
+  return slots;
+}
+
+int depth_lanes(const vr::RenderParams &P) {
+  if (const char *ev = std::getenv("VR_DEPTH_LANES")) {
+    const int k = std::atoi(ev);
+    if (k == 1 || k == 2 || k == 4 || k == 8) return k;
+  }
+  const double waves = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0);  // at K = 1
+  const double rounds = waves / device_wave_slots();
+  return rounds >= VR_DEPTH_ROUNDS_K1 ? 1 : rounds >= VR_DEPTH_ROUNDS_K2 ? 2 : 4;
+}
+
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
               unsigned long long *d_steps, hipStream_t stream, Frame &F) {
@@ -631,10 +672,13 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     if (g_tex.gvec) P.gvec = g_tex.gvec->ptr;
   }
   if (march) {
-    if (P.fast_shade)
-      VR_HIP(vr::fast::launch_march(P, F.mode, F.ab_alias, F.share, F.big, stream));
-    else
-      VR_HIP(vr::exact::launch_march(P, F.mode, F.ab_alias, F.share, F.big, stream));
+    const int K = P.steps ? 1 : depth_lanes(P);  // the counter variant exists for K = 1
+    typedef hipError_t (*launch_fn)(const vr::RenderParams &, int, bool, bool, bool, hipStream_t);
+    static const launch_fn fns[2][4] = {
+        {vr::exact::launch_march_k1, vr::exact::launch_march_k2, vr::exact::launch_march_k4, vr::exact::launch_march_k8},
+        {vr::fast::launch_march_k1, vr::fast::launch_march_k2, vr::fast::launch_march_k4, vr::fast::launch_march_k8}};
+    const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
+    VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
   }

@@ -33,6 +33,33 @@ namespace fast {
 namespace exact {
 #endif
 
+// Depth lanes: each object file is built for one K = VR_MARCH_K (Makefile).  A wave
+// marches 64 / K rays with K lanes per ray; per iteration the K lanes of a ray take its next K
+// consecutive samples and then composite them in order.  K = 1 is the plain one-lane-per-ray march.
+#ifndef VR_MARCH_K
+#define VR_MARCH_K 1
+#endif
+#define VR_CAT2(a, b) a##b
+#define VR_CAT(a, b) VR_CAT2(a, b)
+
+// Value of lane (group base + I) of this lane's K-lane group.  K = 2, 4: one DPP quad_perm move;
+// K = 8: ds_swizzle in 32-lane bit mode (and 0x18, or I).
+template <int K, int I>
+__device__ __forceinline__ float group_lane(float v) {
+  if constexpr (K == 1) {
+    return v;
+  } else if constexpr (K == 2) {
+    constexpr int ctrl = I | (I << 2) | ((2 + I) << 4) | ((2 + I) << 6);
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false));
+  } else if constexpr (K == 4) {
+    constexpr int ctrl = I | (I << 2) | (I << 4) | (I << 6);
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false));
+  } else {
+    static_assert(K == 8, "depth lanes: K in {1, 2, 4, 8}");
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (I << 5)));
+  }
+}
+
 // Per-lane march state carried across chunks.
 struct Ray {
   f3 o, pos, step;
@@ -46,17 +73,126 @@ struct ChunkStats {
   uint32_t staged, leap, fall, iter, lit;
 };
 
+// One sample of a ray at position `pos` (volumeRender_kernel.cu:444-474): the emission /
+// absorption fetch, opacity, and for a lit, non-empty sample the gradient and the shading.  Returns
+// the premultiplied colour (r, g, b) and the opacity; `shaded` says whether shading ran.
+template <int MODE, bool AB_ALIAS, bool SHARE2, bool BIG, bool NANCHK>
+__device__ __forceinline__ void sample_at(const RenderParams &P, const float *L, const Box &B, bool staged,
+                                          const f3 pos, const f3 o, float &r, float &gg, float &b, float &alpha,
+                                          bool &shaded) {
+  const DevTex &E = P.em;
+  const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
+  const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
+  const float tstep = P.tstep;
+  const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
+  // unclamped axes (axis_raw): exact on the LDS path, clamped by fetch_at on the global one
+  const Ax ax = axis_raw<NANCHK>(ps.x, E.fnx), ay = axis_raw<NANCHK>(ps.y, E.fny),
+           az = axis_raw<NANCHK>(ps.z, E.fnz);
+  // centre cell in the slot; the gradient taps below differ from it along one axis only
+  const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
+  const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
+  const int ayz = lz * B.pxy + ly * B.px;  // slot word of (0, ly, lz)
+  const int ac = ayz + lx;
+  const float em_s = fetch_at<BIG>(E, L, B, staged && inx && iny && inz, ac, ax, ay, az);
+  const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
+  const float e = P.fe * em_s;
+  const float a = P.fa * ab_s;
+  alpha = opacity<VR_MARCH_FAST>(a, tstep);
+  const float eds = e * tstep;
+  float ir = 0.f, ig = 0.f, ib = 0.f;
+  const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
+  shaded = MODE != 0 && !skip;
+  if (MODE != 0 && !skip) {
+    f3 g;
+    if (MODE == 1 && (VR_ABLATE & 4)) {
+      g = mk(ps.x, ps.y, em_s);
+    } else if (MODE == 1) {  // computeGradient on tex_emission (gem == em), world offsets +-gstep
+      const float xp = ((pos.x + P.gstep[0]) - bmin.x) * bsc.x;
+      const float xm = ((pos.x - P.gstep[0]) - bmin.x) * bsc.x;
+      const float yp = ((pos.y + P.gstep[1]) - bmin.y) * bsc.y;
+      const float ym = ((pos.y - P.gstep[1]) - bmin.y) * bsc.y;
+      const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
+      const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
+      const bool syz = staged && iny && inz, sxz = staged && inx && inz, sxy = staged && inx && iny;
+      const Ax axp = axis_raw<NANCHK>(xp, E.fnx), axm = axis_raw<NANCHK>(xm, E.fnx);
+      const int lxp = slot_coord(axp.i, B.rx), lxm = slot_coord(axm.i, B.rx);
+      g.x = fetch_at<BIG>(E, L, B, syz && in_box(lxp, B.ex), ayz + lxp, axp, ay, az) -
+            fetch_at<BIG>(E, L, B, syz && in_box(lxm, B.ex), ayz + lxm, axm, ay, az);
+      const Ax ayp = axis_raw<NANCHK>(yp, E.fny), aym = axis_raw<NANCHK>(ym, E.fny);
+      const int lyp = slot_coord(ayp.i, B.ry), lym = slot_coord(aym.i, B.ry);
+      const int axz = lz * B.pxy + lx;
+      g.y = fetch_at<BIG>(E, L, B, sxz && in_box(lyp, B.ey), axz + lyp * B.px, ax, ayp, az) -
+            fetch_at<BIG>(E, L, B, sxz && in_box(lym, B.ey), axz + lym * B.px, ax, aym, az);
+      const Ax azp = axis_raw<NANCHK>(zp, E.fnz), azm = axis_raw<NANCHK>(zm, E.fnz);
+      const int lzp = slot_coord(azp.i, B.rz), lzm = slot_coord(azm.i, B.rz);
+      const int axy = ly * B.px + lx;
+      g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
+            fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
+      g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
+    } else if (SHARE2) {
+      const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
+      if (P.gvec)
+        g = fetch_vec<BIG>(P.gvec, P.gx, cx, cy, cz);
+      else
+        g = mk(fetch<BIG>(P.gx, cx, cy, cz), fetch<BIG>(P.gy, cx, cy, cz), fetch<BIG>(P.gz, cx, cy, cz));
+    } else {
+      g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
+             tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
+    }
+    const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
+    shade_lights<VR_MARCH_FAST>(P, g, pos, o, refl, ir, ig, ib);
+  }
+  r = fmaf(eds, P.color[0], ir) * alpha;
+  gg = fmaf(eds, P.color[1], ig) * alpha;
+  b = fmaf(eds, P.color[2], ib) * alpha;
+}
+
+// Front-to-back compositing of one sample and the march recurrences of volumeRender_kernel.cu:
+// 476-492, in the reference's order: early exit on sum.a > thr before t > tfar; pos += step only
+// while the ray goes on.
+__device__ __forceinline__ void composite(const RenderParams &P, Ray &R, float r, float gg, float b, float alpha) {
+  const float om = 1.f - R.sa;
+  R.sr = fmaf(om, r, R.sr);
+  R.sg = fmaf(om, gg, R.sg);
+  R.sb = fmaf(om, b, R.sb);
+  R.sa = fmaf(om, alpha, R.sa);
+  ++R.nsteps;
+  if (R.sa > P.thr || R.nsteps >= P.max_steps) {
+    R.alive = false;
+  } else {
+    R.t += P.tstep;
+    if (R.t > R.tfar) R.alive = false;
+    else R.pos = mk(R.pos.x + R.step.x, R.pos.y + R.step.y, R.pos.z + R.step.z);
+  }
+}
+
+// Composite the K samples of a depth-lane group in order (every lane of the group does it).
+template <int K, int I>
+__device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, float r, float gg, float b,
+                                                float alpha) {
+  if constexpr (I < K) {
+    const float ri = group_lane<K, I>(r), gi = group_lane<K, I>(gg), bi = group_lane<K, I>(b),
+                ai = group_lane<K, I>(alpha);
+    if (R.alive) composite(P, R, ri, gi, bi, ai);
+    composite_group<K, I + 1>(P, R, r, gg, b, alpha);
+  }
+}
+
 // The chunked march of one wave.  NANCHK = false when every live ray of the wave has a finite
 // start position and step: all volume coordinates are then finite and the NaN -> 0 substitution
 // of the sampler is skipped (the LUT coordinates, which are NaN for a zero gradient, keep it).
 // MODE 0: no lights; 1: on-the-fly gradient from the staged emission texture (gem == em);
 // 2: lookup gradient (gx/gy/gz from global memory, at the centre's axes when SHARE2).
-template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP>
+// K > 1 (depth lanes): the K lanes of a ray hold identical ray state; lane `sub` takes sample
+// sub of each group of K, at the position the reference's recurrence gives it (the same adds the
+// compositing replays), and every lane composites the K samples in order, so the result is the
+// same bits as K = 1.  Samples past an early exit are computed and discarded.
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
+  static_assert(!COUNT || K == 1, "the counter variant is built for K = 1 only");
   const DevTex &E = P.em;
-  const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
-  const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
-  const float tstep = P.tstep, thr = P.thr;
+  const float tstep = P.tstep;
+  const int sub = lane & (K - 1);
 
   while (__any(R.alive)) {
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
@@ -85,85 +221,41 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     }
 
     // ---- S samples ---------------------------------------------------------------------------
-    for (int k = 0; k < S && R.alive; ++k) {
-      const f3 pos = R.pos;
-      const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
-      // unclamped axes (axis_raw): exact on the LDS path, clamped by fetch_at on the global one
-      const Ax ax = axis_raw<NANCHK>(ps.x, E.fnx), ay = axis_raw<NANCHK>(ps.y, E.fny),
-               az = axis_raw<NANCHK>(ps.z, E.fnz);
-      // centre cell in the slot; the gradient taps below differ from it along one axis only
-      const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
-      const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
-      const int ayz = lz * B.pxy + ly * B.px;  // slot word of (0, ly, lz)
-      const int ac = ayz + lx;
-      const float em_s = fetch_at<BIG>(E, L, B, staged && inx && iny && inz, ac, ax, ay, az);
-      const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
-      const float e = P.fe * em_s;
-      const float a = P.fa * ab_s;
-      const float alpha = opacity<VR_MARCH_FAST>(a, tstep);
-      const float eds = e * tstep;
-      float ir = 0.f, ig = 0.f, ib = 0.f;
-      const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
-      if (COUNT) {
-        ++C.iter;
-        C.lit += (MODE != 0 && __any(!skip)) ? 1u : 0u;
-      }
-      if (MODE != 0 && !skip) {
-        if (COUNT) ++R.nlit;
-        f3 g;
-        if (MODE == 1 && (VR_ABLATE & 4)) {
-          g = mk(ps.x, ps.y, em_s);
-        } else if (MODE == 1) {  // computeGradient on tex_emission (gem == em), world offsets +-gstep
-          const float xp = ((pos.x + P.gstep[0]) - bmin.x) * bsc.x;
-          const float xm = ((pos.x - P.gstep[0]) - bmin.x) * bsc.x;
-          const float yp = ((pos.y + P.gstep[1]) - bmin.y) * bsc.y;
-          const float ym = ((pos.y - P.gstep[1]) - bmin.y) * bsc.y;
-          const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
-          const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
-          const bool syz = staged && iny && inz, sxz = staged && inx && inz, sxy = staged && inx && iny;
-          const Ax axp = axis_raw<NANCHK>(xp, E.fnx), axm = axis_raw<NANCHK>(xm, E.fnx);
-          const int lxp = slot_coord(axp.i, B.rx), lxm = slot_coord(axm.i, B.rx);
-          g.x = fetch_at<BIG>(E, L, B, syz && in_box(lxp, B.ex), ayz + lxp, axp, ay, az) -
-                fetch_at<BIG>(E, L, B, syz && in_box(lxm, B.ex), ayz + lxm, axm, ay, az);
-          const Ax ayp = axis_raw<NANCHK>(yp, E.fny), aym = axis_raw<NANCHK>(ym, E.fny);
-          const int lyp = slot_coord(ayp.i, B.ry), lym = slot_coord(aym.i, B.ry);
-          const int axz = lz * B.pxy + lx;
-          g.y = fetch_at<BIG>(E, L, B, sxz && in_box(lyp, B.ey), axz + lyp * B.px, ax, ayp, az) -
-                fetch_at<BIG>(E, L, B, sxz && in_box(lym, B.ey), axz + lym * B.px, ax, aym, az);
-          const Ax azp = axis_raw<NANCHK>(zp, E.fnz), azm = axis_raw<NANCHK>(zm, E.fnz);
-          const int lzp = slot_coord(azp.i, B.rz), lzm = slot_coord(azm.i, B.rz);
-          const int axy = ly * B.px + lx;
-          g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
-                fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
-          g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
-        } else if (SHARE2) {
-          const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
-          if (P.gvec)
-            g = fetch_vec<BIG>(P.gvec, P.gx, cx, cy, cz);
-          else
-            g = mk(fetch<BIG>(P.gx, cx, cy, cz), fetch<BIG>(P.gy, cx, cy, cz), fetch<BIG>(P.gz, cx, cy, cz));
-        } else {
-          g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
-                 tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
+    if constexpr (K == 1) {
+      for (int k = 0; k < S && R.alive; ++k) {
+        float r, gg, b, alpha;
+        bool shaded;
+        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
+        if (COUNT) {
+          ++C.iter;
+          C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
+          R.nlit += shaded ? 1 : 0;
         }
-        const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
-        shade_lights<VR_MARCH_FAST>(P, g, pos, R.o, refl, ir, ig, ib);
+        composite(P, R, r, gg, b, alpha);
       }
-      const float r = fmaf(eds, P.color[0], ir) * alpha;
-      const float gg = fmaf(eds, P.color[1], ig) * alpha;
-      const float b = fmaf(eds, P.color[2], ib) * alpha;
-      const float om = 1.f - R.sa;
-      R.sr = fmaf(om, r, R.sr);
-      R.sg = fmaf(om, gg, R.sg);
-      R.sb = fmaf(om, b, R.sb);
-      R.sa = fmaf(om, alpha, R.sa);
-      ++R.nsteps;
-      if (R.sa > thr || R.nsteps >= P.max_steps) {
-        R.alive = false;
-      } else {
-        R.t += tstep;
-        if (R.t > R.tfar) R.alive = false;
-        else R.pos = mk(pos.x + R.step.x, pos.y + R.step.y, pos.z + R.step.z);
+    } else {
+      for (int k = 0; k < S && R.alive; k += K) {
+        // this lane's sample: `sub` steps of the reference recurrence from the ray's position,
+        // valid while the t / step-cap exits of the earlier samples have not fired
+        f3 q = R.pos, mp = R.pos;
+        float tt = R.t;
+        bool v = true, mv = true;
+#pragma unroll
+        for (int i = 0; i < K - 1; ++i) {
+          tt += tstep;
+          v = v && (R.nsteps + i + 1 < P.max_steps) && !(tt > R.tfar);
+          q = mk(q.x + R.step.x, q.y + R.step.y, q.z + R.step.z);
+          if (i + 1 == sub) {
+            mp = q;
+            mv = v;
+          }
+        }
+        float r = 0.f, gg = 0.f, b = 0.f, alpha = 0.f;
+        if (mv) {
+          bool shaded;
+          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, mp, R.o, r, gg, b, alpha, shaded);
+        }
+        composite_group<K, 0>(P, R, r, gg, b, alpha);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -178,20 +270,29 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif
 
-// One wave marches one 8x8-pixel tile (lane -> (x = lane >> 3, y = lane & 7)).  Tile t is quadrant
-// (t & 3) of 16x16 block (t >> 2), blocks row-major, t = blockIdx.x * VR_WG_WAVES + wave.  With
-// single-wave workgroups a wave whose rays end early releases its LDS slot at once instead of
-// holding it until the slowest wave of a larger workgroup has finished.
-template <int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP>
+// One wave marches one tile of 64 / K rays (K = 1: 8x8 pixels, 2: 4x8, 4: 4x4, 8: 2x4; lane ->
+// ray lane / K, ray -> (x = ray / th, y = ray % th)).  Tile t is quadrant (t & 3) of block
+// (t >> 2), a block being 2x2 tiles (16x16 pixels at K = 1), blocks row-major,
+// t = blockIdx.x * VR_WG_WAVES + wave.
+template <int K>
+struct TileShape {
+  static constexpr int LR = (K == 1 ? 6 : K == 2 ? 5 : K == 4 ? 4 : 3);  // log2 rays per wave
+  static constexpr int LK = 6 - LR;                                         // log2 K
+  static constexpr int TW = 1 << (LR / 2), TH = 1 << (LR - LR / 2);       // tile width, height
+};
+
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP>
 __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderParams P) {
+  using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
   const int tile = blockIdx.x * VR_WG_WAVES + wave;
-  const int nbx = (P.part_cols + 15) >> 4;
-  const int blk16 = tile >> 2, quad = tile & 3;
-  const int lc = (blk16 % nbx) * 16 + (quad & 1) * 8 + (lane >> 3);
-  const int y = (blk16 / nbx) * 16 + (quad >> 1) * 8 + (lane & 7);
+  const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
+  const int blk = tile >> 2, quad = tile & 3;
+  const int ray = lane >> TS::LK;
+  const int lc = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + (ray / TS::TH);
+  const int y = (blk / nbx) * (2 * TS::TH) + (quad >> 1) * TS::TH + (ray % TS::TH);
   const bool active = (lc < P.part_cols) && (y < P.height);
   Ray R;
   R.o = mk(0.f, 0.f, 0.f);
@@ -215,11 +316,11 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderPar
   }
   // every coordinate the march forms from a finite start and step is finite
   if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
   else
-    march<MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
-  if (active) {
+  if (active && (lane & (K - 1)) == 0) {
     const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
     const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
     P.out[kk] = R.sr;
@@ -247,13 +348,14 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderPar
 
 template <int MODE, bool AB, bool SH, int CAP>
 static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
+  constexpr int K = VR_MARCH_K;
   const dim3 blk(64 * VR_WG_WAVES);
-  if (P.steps) {
-    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, true, CAP>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<MODE, AB, true, SH, false, CAP>), grid, blk, 0, s, P);
+  if (K == 1 && P.steps) {
+    if (big) hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, true, CAP>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, false, CAP>), grid, blk, 0, s, P);
   } else {
-    if (big) hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, true, CAP>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<MODE, AB, false, SH, false, CAP>), grid, blk, 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP>), grid, blk, 0, s, P);
   }
   return hipGetLastError();
 }
@@ -264,11 +366,17 @@ static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool
                      : launch_c<MODE, AB, SH, VR_LDS_CAP>(P, grid, s, big);
 }
 
-// Host entry: the staged kernel needs a bound, non-constant emission texture; for MODE 1 the
-// gradient texture must be the emission texture itself (the reference's tex_emission binding).
-hipError_t launch_march(const RenderParams &P, int mode, bool ab_alias, bool share, bool big, hipStream_t s) {
+// Host entry (launch_march_k1 / _k2 / _k4 / _k8, one per object file): the staged kernel needs a
+// bound, non-constant emission texture; for MODE 1 the gradient texture must be the emission
+// texture itself (the reference's tex_emission binding).  The counter variant (P.steps) exists
+// for K = 1 only; the host routes counted launches there.
+hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, bool ab_alias, bool share, bool big,
+                                              hipStream_t s) {
+  using TS = TileShape<VR_MARCH_K>;
   if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
-  const uint64_t tiles = (uint64_t)((P.part_cols + 15) / 16) * (uint64_t)((P.height + 15) / 16) * 4;
+  if (VR_MARCH_K != 1 && P.steps) return hipErrorInvalidValue;
+  const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
+                         (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES));
   switch (mode) {
     case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);
