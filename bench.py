@@ -218,7 +218,8 @@ def main():
                                    + ", rotate(125,25,0) f=3 dist=6 thr=0.9",
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
-                       + (" + RCCL gather" if world > 1 else "")},
+                       + (" + RCCL gather" if world > 1 else ""),
+                       "depth_lanes": mex.depth_lanes(my_cols, H)},
             "samples_per_frame": total_samples,
             "shaded_samples_per_frame": total_lit,
             "chunks_staged_leaped_global": chunk_stats,

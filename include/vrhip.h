@@ -138,6 +138,11 @@ int64_t vr_partition_columns(int64_t w, const vr_partition *part);
 int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t block_cols,
                            int32_t num_parts, int64_t max_cols, float *d_out, void *stream);
 
+/* Depth lanes (lanes per ray) the march kernel uses for a launch of part_cols x
+ * height rays on the current device: 1, 2, 4 or 8 (VR_DEPTH_LANES overrides).  Launches with few
+ * waves per wave slot of the device also follow a longest-first workgroup schedule. */
+int vr_depth_lanes(int64_t part_cols, int64_t height);
+
 /* Synthetic test volume V_shell(n) of SURVEY.md 8d, generated on the device into d_out[n^3]. */
 int vr_synth_shell_device(float *d_out, uint64_t n, void *stream);
 

@@ -341,7 +341,8 @@ def test_step_count_matches_oracle(counter_clock):
 @pytest.mark.parametrize("scene", ["hg2", "lookup", "ea"])
 def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, shade):
     """The LDS-staged march, the plain kernel, the empty-sample skip / empty-chunk leap and the
-    XCD tile order and the depth lanes (K lanes per ray compositing K consecutive samples) change
+    XCD tile order, the longest-first workgroup schedule (every repeated frame shape after the first
+    launch) and the depth lanes (K lanes per ray compositing K consecutive samples) change
     only where data comes from, which exact no-ops are elided and which lane computes a sample:
     the images must agree bit for bit, with either shading arithmetic.  The image
     size is ragged for every tile shape."""
@@ -355,7 +356,7 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
     keys = ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT",
-            "VR_NO_GVEC", "VR_DEPTH_LANES")
+            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED")
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
@@ -363,7 +364,9 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
                       ("k1", {"VR_DEPTH_LANES": "1"}), ("k2", {"VR_DEPTH_LANES": "2"}), ("k4", {"VR_DEPTH_LANES": "4"}),
                       ("k8", {"VR_DEPTH_LANES": "8"}), ("k2_noskip", {"VR_DEPTH_LANES": "2", "VR_NO_EMPTY_SKIP": "1"}),
                       ("k8_wide", {"VR_DEPTH_LANES": "8", "VR_WIDE_SLOT": "1"}),
-                      ("k4_big", {"VR_DEPTH_LANES": "4", "VR_FORCE_BIG": "1"})]:
+                      ("k4_big", {"VR_DEPTH_LANES": "4", "VR_FORCE_BIG": "1"}),
+                      ("nosched", {"VR_SCHED": "0"}), ("k2_sched", {"VR_DEPTH_LANES": "2", "VR_SCHED": "1"}),
+                      ("k1_sched", {"VR_DEPTH_LANES": "1", "VR_SCHED": "1"})]:
         for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():

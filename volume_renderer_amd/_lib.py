@@ -64,6 +64,7 @@ SIGNATURES = [
     ("vr_partition_columns", c_int64, [c_int64, POINTER(VrPartition)]),
     ("vr_assemble_partitions", c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int64, c_void_p,
                                        c_void_p]),
+    ("vr_depth_lanes", c_int, [c_int64, c_int64]),
     ("vr_synth_shell_device", c_int, [c_void_p, c_uint64, c_void_p]),
     ("vr_gradient_device", c_int, [c_void_p, POINTER(c_uint64), c_void_p, c_void_p, c_void_p, c_void_p]),
     ("vr_debug_slot_transition", c_int, [POINTER(c_int32), c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,

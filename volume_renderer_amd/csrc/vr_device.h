@@ -63,6 +63,13 @@ struct RenderParams {
   int32_t block_cols, part, num_parts, part_cols;
   int32_t plane_cols;             // column stride of the output planes (part 0's column count)
   float *out;                     // [3][plane_cols][H]: column-major planar image of the part
+  // launch schedule: workgroup b marches tile block wg_order[b] (null: b); each
+  // block's duration in s_memrealtime ticks is stored to wg_cost[block] (null: not recorded)
+  const uint32_t *wg_order;
+  uint32_t *wg_cost;
+  uint32_t sched_blocks;          // length of wg_order / wg_cost (must equal the launch's grid)
+  uint32_t prio_blocks;           // scheduled launch: the first prio_blocks workgroups (the longest)
+                                  // run at raised wave priority
   unsigned long long *steps;      // optional sample counter
 };
 

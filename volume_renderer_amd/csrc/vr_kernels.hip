@@ -347,6 +347,52 @@ hipError_t launch_interleave3(const float *a, const float *b, const float *c, fl
   return hipGetLastError();
 }
 
+// Longest-first schedule of the march workgroups: order[] lists the tile blocks by
+// their last measured duration, longest first, in 256 log-spaced buckets (8 per octave; order
+// within a bucket is arbitrary).  The march writes the same image for any order.  One workgroup.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t c) {
+  if (c == 0) return 0;
+  const uint32_t lz = __clz(c), e = 31u - lz;                        // floor(log2 c)
+  const uint32_t m = e >= 3 ? (c >> (e - 3)) & 7u : (c << (3 - e)) & 7u;  // next 3 bits
+  return min(255u, e * 8u + m);
+}
+
+__global__ __launch_bounds__(1024) void order_kernel(const uint32_t *__restrict__ cost, uint32_t n,
+                                                     uint32_t *__restrict__ order) {
+  __shared__ uint32_t hist[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive offsets, largest bucket first
+    uint32_t acc = 0;
+    for (int b = 255; b >= 0; --b) {
+      const uint32_t c = hist[b];
+      hist[b] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
+}
+
+hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void iota_kernel(uint32_t *__restrict__ order, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) order[i] = i;
+}
+
+hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, s, order, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s) {
   const uint64_t total = n * n * n;
   if (!total) return hipSuccess;

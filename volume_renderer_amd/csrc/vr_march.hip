@@ -16,6 +16,24 @@
 #include <stdint.h>
 #include <math.h>
 
+#ifndef VR_MARCH_K
+#define VR_MARCH_K 1  // depth lanes of this object file (see below)
+#endif
+#ifndef VR_BRANCHFREE_LEAP
+#define VR_BRANCHFREE_LEAP 1  // empty-chunk leap of K = 1 lanes without per-step branches
+#endif
+#ifndef VR_CHUNK_PER_LANE
+#define VR_CHUNK_PER_LANE 16  // chunk length per depth lane for K >= 2 (samples per ray per chunk)
+#endif
+#ifndef VR_CHUNK
+// samples per ray per staged chunk: the chunk set-up (box reduction + staging copy) is paid once
+// per S / K iterations, so longer chunks for more depth lanes (fewer rays -> thinner boxes)
+#define VR_CHUNK (VR_MARCH_K >= 2 ? VR_CHUNK_PER_LANE * VR_MARCH_K : 32)
+#endif
+// the host's staging halo covers chunks of up to this many sequential position additions
+// (vr_capi.hip chunk_samples): a longer chunk could leap over a tap outside its staged box
+static_assert(VR_CHUNK <= (VR_MARCH_K >= 2 ? 16 * VR_MARCH_K : 32), "chunk longer than the host's halo margin");
+
 #include "vr_device.h"
 #include "vr_sampling.h"
 #include "vr_stage.h"
@@ -36,9 +54,6 @@ namespace exact {
 // Depth lanes: each object file is built for one K = VR_MARCH_K (Makefile).  A wave
 // marches 64 / K rays with K lanes per ray; per iteration the K lanes of a ray take its next K
 // consecutive samples and then composite them in order.  K = 1 is the plain one-lane-per-ray march.
-#ifndef VR_MARCH_K
-#define VR_MARCH_K 1
-#endif
 #define VR_CAT2(a, b) a##b
 #define VR_CAT(a, b) VR_CAT2(a, b)
 
@@ -67,6 +82,7 @@ struct Ray {
   float sr, sg, sb, sa;
   int32_t nsteps, nlit;
   bool alive;
+  bool mine;  // K > 1: this lane's current sample exists (see march)
 };
 
 struct ChunkStats {
@@ -166,15 +182,31 @@ __device__ __forceinline__ void composite(const RenderParams &P, Ray &R, float r
   }
 }
 
-// Composite the K samples of a depth-lane group in order (every lane of the group does it).
+// Whether any lane of this lane's K-lane group has b set.
+template <int K>
+__device__ __forceinline__ bool group_any(bool b) {
+  const uint64_t m = __ballot(b);
+  const int base = (int)(__lane_id() & ~(uint32_t)(K - 1));
+  return ((m >> base) & ((1ull << K) - 1)) != 0ull;
+}
+
+// Composite the existing samples (a prefix of nv of the K) of a depth-lane group in order, every
+// lane of the group alike; the ray stops at the first sum.a > thr (volumeRender_kernel.cu:482).
 template <int K, int I>
-__device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, float r, float gg, float b,
+__device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, int nv, float r, float gg, float b,
                                                 float alpha) {
   if constexpr (I < K) {
     const float ri = group_lane<K, I>(r), gi = group_lane<K, I>(gg), bi = group_lane<K, I>(b),
                 ai = group_lane<K, I>(alpha);
-    if (R.alive) composite(P, R, ri, gi, bi, ai);
-    composite_group<K, I + 1>(P, R, r, gg, b, alpha);
+    if (I < nv && R.alive) {
+      const float om = 1.f - R.sa;
+      R.sr = fmaf(om, ri, R.sr);
+      R.sg = fmaf(om, gi, R.sg);
+      R.sb = fmaf(om, bi, R.sb);
+      R.sa = fmaf(om, ai, R.sa);
+      if (R.sa > P.thr) R.alive = false;
+    }
+    composite_group<K, I + 1>(P, R, nv, r, gg, b, alpha);
   }
 }
 
@@ -183,16 +215,25 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // of the sampler is skipped (the LUT coordinates, which are NaN for a zero gradient, keep it).
 // MODE 0: no lights; 1: on-the-fly gradient from the staged emission texture (gem == em);
 // 2: lookup gradient (gx/gy/gz from global memory, at the centre's axes when SHARE2).
-// K > 1 (depth lanes): the K lanes of a ray hold identical ray state; lane `sub` takes sample
-// sub of each group of K, at the position the reference's recurrence gives it (the same adds the
-// compositing replays), and every lane composites the K samples in order, so the result is the
-// same bits as K = 1.  Samples past an early exit are computed and discarded.
+// K > 1 (depth lanes): lane `sub` of a ray's group owns samples sub, sub + K, sub + 2K, ...: its
+// pos / t / nsteps (= sample index) follow the reference's recurrence from the ray start (sub
+// steps, then K per iteration: the same sequence of rounded additions as one lane taking every
+// sample), and `mine` says whether its sample exists (t <= tfar and index < max_steps; t is
+// non-decreasing, so the existing samples of a group are a prefix).  Per iteration each lane
+// takes its sample, then every lane composites the group's samples in order; `alive` (the ray:
+// not stopped by sum.a > thr and some sample left) is the same in all K lanes.  Bit-identical to
+// K = 1; samples after an early exit are computed and discarded.
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
   static_assert(!COUNT || K == 1, "the counter variant is built for K = 1 only");
   const DevTex &E = P.em;
-  const float tstep = P.tstep;
   const int sub = lane & (K - 1);
+  if constexpr (K > 1) {
+    R.nsteps = 0;
+    R.mine = R.alive;
+    leap(P, sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to this lane's first sample
+    R.alive = group_any<K>(R.mine);
+  }
 
   while (__any(R.alive)) {
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
@@ -200,7 +241,8 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     bool staged, partial;
     Box B;
     int box_vol = 0;
-    plan_chunk<CAP>(P, R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B, COUNT ? &box_vol : nullptr);
+    plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B,
+                    COUNT ? &box_vol : nullptr);
     if (COUNT && lane == 0) {  // diagnostics: box volume of partial/failed chunks, S of staged ones
       if (!staged || partial) atomicAdd(P.steps + 8 + min(box_vol >> 8, 31), 1ull);
       else atomicAdd(P.steps + 40 + (S >= 32 ? 0 : (S >= 16 ? 1 : (S >= 8 ? 2 : 3))), 1ull);
@@ -216,7 +258,13 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     if (COUNT) ++(staged && !partial ? (empty ? C.leap : C.staged) : C.fall);
 
     if (empty) {
-      leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
+      if constexpr (K == 1) {
+        if (COUNT || !VR_BRANCHFREE_LEAP) leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);  // exact counts
+        else advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
+      } else {
+        advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        R.alive = R.alive && group_any<K>(R.mine);
+      }
       continue;
     }
 
@@ -235,27 +283,16 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       }
     } else {
       for (int k = 0; k < S && R.alive; k += K) {
-        // this lane's sample: `sub` steps of the reference recurrence from the ray's position,
-        // valid while the t / step-cap exits of the earlier samples have not fired
-        f3 q = R.pos, mp = R.pos;
-        float tt = R.t;
-        bool v = true, mv = true;
-#pragma unroll
-        for (int i = 0; i < K - 1; ++i) {
-          tt += tstep;
-          v = v && (R.nsteps + i + 1 < P.max_steps) && !(tt > R.tfar);
-          q = mk(q.x + R.step.x, q.y + R.step.y, q.z + R.step.z);
-          if (i + 1 == sub) {
-            mp = q;
-            mv = v;
-          }
-        }
         float r = 0.f, gg = 0.f, b = 0.f, alpha = 0.f;
-        if (mv) {
+        if (R.mine) {
           bool shaded;
-          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, mp, R.o, r, gg, b, alpha, shaded);
+          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
         }
-        composite_group<K, 0>(P, R, r, gg, b, alpha);
+        const uint64_t m = __ballot(R.mine);
+        const int nv = __popcll((m >> (lane & ~(K - 1))) & ((1ull << K) - 1));  // existing samples
+        composite_group<K, 0>(P, R, nv, r, gg, b, alpha);
+        advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to sample + K
+        R.alive = R.alive && group_any<K>(R.mine);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -281,13 +318,19 @@ struct TileShape {
   static constexpr int TW = 1 << (LR / 2), TH = 1 << (LR - LR / 2);       // tile width, height
 };
 
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP>
+// SCHED: the launch follows P.wg_order and records each block's duration in P.wg_cost (a
+// separate instantiation: the hooks cost ~4 % when compiled in, even unused).
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, bool SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
-  const int tile = blockIdx.x * VR_WG_WAVES + wave;
+  const uint64_t clk0 = SCHED ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint32_t wg = SCHED ? P.wg_order[blockIdx.x] : blockIdx.x;  // cost-ordered schedule
+  // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
+  if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
+  const int tile = (int)wg * VR_WG_WAVES + wave;
   const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
   const int blk = tile >> 2, quad = tile & 3;
   const int ray = lane >> TS::LK;
@@ -327,6 +370,13 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderPar
     P.out[kk + plane] = R.sg;
     P.out[kk + 2 * plane] = R.sb;
   }
+  if (SCHED) {  // this block's duration, for the next launch's schedule
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
+      P.wg_cost[wg] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+    }
+  }
   if (COUNT) {
     unsigned long long s = (unsigned long long)R.nsteps, l = (unsigned long long)R.nlit;
 #pragma unroll
@@ -350,12 +400,16 @@ template <int MODE, bool AB, bool SH, int CAP>
 static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
   constexpr int K = VR_MARCH_K;
   const dim3 blk(64 * VR_WG_WAVES);
+  const bool sched = P.wg_order && P.wg_cost;
   if (K == 1 && P.steps) {
-    if (big) hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, true, CAP>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, false, CAP>), grid, blk, 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, true, CAP, false>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, false, CAP, false>), grid, blk, 0, s, P);
+  } else if (K > 1 && sched) {  // scheduled launches use depth lanes (few waves per slot)
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, (K > 1)>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, (K > 1)>), grid, blk, 0, s, P);
   } else {
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP>), grid, blk, 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, false>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, false>), grid, blk, 0, s, P);
   }
   return hipGetLastError();
 }
@@ -370,6 +424,15 @@ static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool
 // bound, non-constant emission texture; for MODE 1 the gradient texture must be the emission
 // texture itself (the reference's tex_emission binding).  The counter variant (P.steps) exists
 // for K = 1 only; the host routes counted launches there.
+// Number of workgroups launch_march_k<K> uses for this frame (the schedule's length).
+uint32_t VR_CAT(march_blocks_k, VR_MARCH_K)(const RenderParams &P) {
+  using TS = TileShape<VR_MARCH_K>;
+  if (P.part_cols <= 0 || P.height <= 0) return 0;
+  const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
+                         (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
+  return (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
+}
+
 hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, bool ab_alias, bool share, bool big,
                                               hipStream_t s) {
   using TS = TileShape<VR_MARCH_K>;
@@ -378,6 +441,8 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
   const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES));
+  if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || VR_MARCH_K == 1))
+    return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {
     case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);
     case 1: return ab_alias ? launch_m<1, true, false>(P, grid, s, big) : launch_m<1, false, false>(P, grid, s, big);

@@ -286,4 +286,17 @@ __device__ __forceinline__ void leap(const RenderParams &P, int S, bool &alive, 
   }
 }
 
+// The same recurrence as leap() for a wave-uniform count, without branches: a lane whose sample
+// stopped existing keeps advancing, but its state is never read again (`alive` stays false), so
+// the live lanes see exactly leap()'s additions.
+__device__ __forceinline__ void advance(const RenderParams &P, int n, bool &alive, int32_t &nsteps, float &t,
+                                        float tfar, f3 &pos, const f3 &step) {
+  for (int k = 0; k < n; ++k) {
+    ++nsteps;
+    t += P.tstep;
+    pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
+    alive = alive && nsteps < P.max_steps && !(t > tfar);
+  }
+}
+
 }  // namespace vr

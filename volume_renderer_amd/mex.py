@@ -175,6 +175,11 @@ def partition_columns(width: int, part) -> int:
     return int(lib().vr_partition_columns(int(width), ctypes.byref(part) if part is not None else None))
 
 
+def depth_lanes(part_cols: int, height: int) -> int:
+    """Depth lanes the march uses for a launch of this shape on the current device (vr_depth_lanes)."""
+    return int(lib().vr_depth_lanes(int(part_cols), int(height)))
+
+
 def render_device(handle, ra: VrRenderArgs, d_out: int, part=None, d_steps: int = 0, stream: int = 0) -> None:
     """'render' into device memory (vr_render_device): asynchronous on `stream`."""
     check(lib().vr_render_device(_handle(handle), ctypes.byref(ra), ctypes.byref(part) if part is not None else None,
