@@ -11,6 +11,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
@@ -37,12 +38,13 @@ with open(os.path.join(out, "pmc_summary.txt"), "w") as fh:
     fh.write("\n".join(lines) + "\n")
 
 
-def mean(kfilter, counter, exclude="<1, true, true"):
-    xs = [v for k, cs in vals.items() if kfilter in k and exclude not in k for v in cs.get(counter, {}).values()]
+def mean(kpattern, counter):
+    xs = [v for k, cs in vals.items() if re.search(kpattern, k) for v in cs.get(counter, {}).values()]
     return sum(xs) / len(xs) if xs else None
 
 
-march = "march_kernel<1, true, false"  # metric config: MODE 1, absorption aliases emission, no counters
+# metric config: march_kernel<K, MODE 1, absorption aliases emission, no counters, -, 32-bit, slot, unscheduled>
+march = r"march_kernel<\d, 1, true, false, false, false, \d+, false>"
 fetch_kb, write_kb = mean(march, "FETCH_SIZE"), mean(march, "WRITE_SIZE")
 if fetch_kb is not None:
     traffic = 2 * 1024 * fetch_kb + 1024 * (write_kb or 0.0)
