@@ -616,7 +616,7 @@ int device_wave_slots() {
       if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
         cus = prop.multiProcessorCount;
     }
-    slots = cus * 16;  // 4 workgroups of 4 waves per CU (10 KiB LDS slots)
+    slots = cus * 16;  // the heuristics' unit: 16 waves per CU (the march runs 20-24 per CU)
   }
   return slots;
 }
@@ -661,7 +661,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   P.tile_mode = 0;
   // wave slot size of the march: the 8x8-ray footprint per chunk grows with the texels a pixel
   // spans at the volume, tau = dist * vw / (W * f) (pixel pitch 2/W on the image plane at f, box
-  // x-extent 2 = vw texels).  Measured: tau 1.07 (1920 px) is fastest with 10 KiB slots, tau 2.0
+  // x-extent 2 = vw texels).  Measured: tau 1.07 (1920 px) is fastest with small slots, tau 2.0
   // (1024 px) 18 % faster with 12 KiB ones.  VR_WIDE_SLOT=0/1 overrides (A/B).
   {
     const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);

@@ -57,7 +57,7 @@ struct RenderParams {
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)
-  int32_t wide_slot;              // march: 12 KiB wave slots instead of 10 KiB (vr_stage.h)
+  int32_t wide_slot;              // march: 12 KiB wave slots instead of 6 KiB (vr_stage.h)
   int32_t fast_shade;             // 1: hardware-rsq shading and exp2 opacity (default); 0: the oracle's ops
   // image-space partition (vr_partition): local column lc -> global column
   int32_t block_cols, part, num_parts, part_cols;

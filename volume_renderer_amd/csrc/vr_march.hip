@@ -303,6 +303,14 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
   return fabsf(v.x) <= 3.4e38f && fabsf(v.y) <= 3.4e38f && fabsf(v.z) <= 3.4e38f;
 }
 
+// Occupancy of the march: 6 KiB wave slots fit 6 workgroups (24 waves) per CU, which 80 VGPRs
+// allow (6 waves per SIMD; ~2 VGPRs spill).  Measured on MI355X: the metric frame 43.8 -> 42.6 ms
+// (K = 2).  A scheduled launch (few rounds, heavy waves first) keeps the uncapped allocation: its
+// longest waves share a SIMD with fewer others (one rank's share at P = 8: 7.2 ms vs 7.7 capped).
+#ifndef VR_MARCH_MIN_EU
+#define VR_MARCH_MIN_EU 6
+#endif
+constexpr int march_min_eu(int cap, bool sched) { return (cap <= 1536 && !sched) ? VR_MARCH_MIN_EU : 1; }
 #ifndef VR_WG_WAVES
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif
@@ -321,7 +329,7 @@ struct TileShape {
 // SCHED: the launch follows P.wg_order and records each block's duration in P.wg_cost (a
 // separate instantiation: the hooks cost ~4 % when compiled in, even unused).
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, bool SCHED>
-__global__ __launch_bounds__(64 * VR_WG_WAVES) void march_kernel(const RenderParams P) {
+__global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
