@@ -399,3 +399,31 @@ def test_exact_shading_matches_oracle(monkeypatch, counter_clock, scene):
     assert tee.renders[0][2]["bit_exact"] > 0.5, tee.renders[0][2]
     assert np.abs(fast - exact).max() <= 1e-2 * exact.max()
     r.delete()
+
+
+def test_unchanged_lut_and_gradients_stay_resident(monkeypatch, counter_clock):
+    """Upload path: the LUT and the lookup-gradient volumes are uploaded again
+    only when the Volume changed (data pointer, TimeLastUpdate, size -- the reference's own dedup
+    identity), not on every render as setIlluminationTexture / setGradientTextures do
+    (volumeRender_kernel.cu:682-722).  White-box check: an in-place edit that bypasses
+    TimeLastUpdate (impossible in MATLAB, whose arrays are copy-on-write) is not picked up, a
+    touch() or VR_ALWAYS_REUPLOAD=1 (the reference's behaviour) is."""
+    monkeypatch.delenv("VR_ALWAYS_REUPLOAD", raising=False)
+    v = vr.Volume(O.shell_volume(40))
+    gx, gy, gz = v.grad()
+    r = ex1_renderer(v, res=(72, 64))
+    r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = gx, gy, gz
+    a = r.render()
+    gx.Data[...] *= -3.0          # in place, TimeLastUpdate unchanged
+    r.VolumeIllumination.Data[...] *= 0.5
+    b = r.render()
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))  # still the resident copies
+    monkeypatch.setenv("VR_ALWAYS_REUPLOAD", "1")
+    c = r.render()
+    assert not np.array_equal(a, c)
+    monkeypatch.delenv("VR_ALWAYS_REUPLOAD")
+    gx.touch()
+    r.VolumeIllumination.touch()
+    d = r.render()
+    assert np.array_equal(c.view(np.uint32), d.view(np.uint32))
+    r.delete()

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""End-to-end timing of the MATLAB-facing host path (SURVEY.md 8d "end-to-end mex-call time",
+8f row 3 "upload path"), run on the GPU box:
+
+  * sync_volumes of a host V_shell(n) volume (H2D + apron padding + statistics): upload GB/s;
+  * one VolumeRender.render (VolumeRender.m:497-583): 'sync_volumes' with the previous sync time
+    (nothing changed) then 'render' through vr_render (the MEX path: LUT/light upload, launch,
+    D2H of the [H, W, 3] image), compute gradient;
+  * the same with the three lookup-gradient volumes as host Volumes (example1_grad.m), whose
+    'sync_volumes' runs setGradientTextures (volumeRender_kernel.cu:703-722).
+
+Each render figure is the median of --reps calls after one warm-up.  Set VR_ALWAYS_REUPLOAD=1 for
+the reference's behaviour (LUT and gradients re-uploaded by every render).
+usage: python tools/e2e_bench.py [--n 1024 --width 1920 --height 1080 --reps 5]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-lookup", action="store_true")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    import volume_renderer_amd as vr
+    from volume_renderer_amd import mex
+    from bench import rotation
+
+    n, W, H = args.n, args.width, args.height
+    t = torch.empty(n * n * n, dtype=torch.float32, device="cuda")
+    mex.synth_shell_device(t.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
+    host = t.cpu().numpy().reshape((n, n, n), order="F")
+    del t
+    torch.cuda.synchronize()
+
+    em = vr.Volume(host)
+    lut = vr.Volume(vr.HenyeyGreenstein(64))
+    refl = vr.Volume(1)
+    lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+    h = vr.volumeRender("new")
+    t0 = time.perf_counter()
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)
+    t_sync = time.perf_counter() - t0
+    R = rotation(125, 25, 0)
+    call = ("render", h, lights, lut, np.float32([1.0, 0.4, 0.6]), np.float32([1, 1, 1]), np.uint64([H, W]),
+            np.flip(R, 0).astype(np.float32), np.float32([0, 3.0, 6.0]), np.float32(0.9), np.float32([1, 1, 0]))
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(args.reps):
+            t1 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t1)
+        return float(np.median(ts)) * 1e3
+
+    t_last = np.uint64(mex.timestamp())
+
+    def p_render(*grads):
+        vr.volumeRender("sync_volumes", h, t_last, em, refl, em, *grads)
+        return vr.volumeRender(*call)
+
+    out = {"volume": n, "image": [W, H], "always_reupload": os.environ.get("VR_ALWAYS_REUPLOAD", "0"),
+           "sync_s": round(t_sync, 3), "sync_GBps": round(host.nbytes / t_sync / 1e9, 2),
+           "p_render_ms": round(med(p_render), 2)}
+    if not args.no_lookup:
+        grads = em.grad() if n <= 256 else _device_grad(host, mex, vr)
+        t0 = time.perf_counter()
+        vr.volumeRender("sync_volumes", h, t_last, em, refl, em, *grads)
+        out["sync_lookup_s"] = round(time.perf_counter() - t0, 3)
+        out["p_render_lookup_ms"] = round(med(lambda: p_render(*grads)), 2)
+    vr.volumeRender("delete", h)
+    print(json.dumps(out), flush=True)
+
+
+def _device_grad(host, mex, vr):
+    """Volume.grad of a large volume via vr_gradient_device, returned as host Volumes."""
+    d = torch.from_numpy(host.reshape(-1, order="F")).cuda()
+    g = [torch.empty_like(d) for _ in range(3)]
+    mex.gradient_device(d.data_ptr(), host.shape, *[x.data_ptr() for x in g], torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return [vr.Volume(x.cpu().numpy().reshape(host.shape, order="F")) for x in g]
+
+
+if __name__ == "__main__":
+    main()

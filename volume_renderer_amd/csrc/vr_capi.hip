@@ -126,6 +126,9 @@ struct DevBuf {
   bool nonfinite = false;
   float maxabs = 0.f;
   uint64_t version = 0;  // bumped by every upload into this buffer
+  // the MATLAB Volume it was uploaded from (VolRec identity: data pointer, TimeLastUpdate, size)
+  const float *src_data = nullptr;
+  uint64_t src_last_update = 0, src_bytes = 0;
   ~DevBuf() {
     if (ptr) {
       int cur = 0;
@@ -216,6 +219,15 @@ void reset_tex_unit() {
 
 bool valid(vr_context *h) { return h && g_contexts.count(h) && h->signature == 0xFF00F0A5u; }
 
+bool env_flag(const char *name) {
+  const char *ev = std::getenv(name);
+  return ev && ev[0] == '1';
+}
+bool env_flag_off(const char *name) {
+  const char *ev = std::getenv(name);
+  return ev && ev[0] == '0';
+}
+
 // syncVolume (kernel.cu:659-672): unbind the texture, drop the old array, upload the volume into a
 // fresh device buffer and bind it.  A buffer nobody else references is overwritten in place.
 void sync_volume(vr_context *h, int tex, int slot) {
@@ -262,8 +274,27 @@ void sync_volume(vr_context *h, int tex, int slot) {
   }
   static uint64_t s_version = 0;
   b->version = ++s_version;
+  b->src_data = v.data;
+  b->src_last_update = v.last_update;
+  b->src_bytes = v.memory_size;
   h->buf[slot] = b;
   g_tex.bind[tex] = b;
+}
+
+// setIlluminationTexture / setGradientTextures (kernel.cu:682-722) re-upload their volume on every
+// call.  Here the upload is skipped when the texture is still bound to a buffer uploaded from the
+// same Volume -- the identity the reference's own dedup uses for the emission / absorption /
+// reflection volumes (data pointer, TimeLastUpdate, size; volumeRender.cpp:24-26).  The image is
+// the same; the LUT (1 MiB) and in lookup mode the three gradient volumes (12 GiB at 1024^3) stop
+// crossing PCIe per render.  VR_ALWAYS_REUPLOAD=1 restores the reference's behaviour.
+void sync_volume_if_changed(vr_context *h, int tex, int slot) {
+  const BufPtr &b = g_tex.bind[tex];
+  const VolRec &v = h->vol[slot];
+  if (b && h->buf[slot] == b && b->device == h->device && v.data && b->src_data == v.data &&
+      b->src_last_update == v.last_update && b->src_bytes == v.memory_size && v.last_update != 0 &&
+      !env_flag("VR_ALWAYS_REUPLOAD"))
+    return;
+  sync_volume(h, tex, slot);
 }
 
 // The decisions of syncWithDevice (kernel.cu:739-867) over an abstract state, so that the real
@@ -362,21 +393,12 @@ void mm_sync(vr_context *h) {
   g_tex.idx_ab = s.idx_ab;
   g_tex.idx_re = s.idx_re;
   if (h->vol[T_DX].last_update != 0 && h->vol[T_DY].last_update != 0 && h->vol[T_DZ].last_update != 0) {
-    // setGradientTextures (kernel.cu:703-722): always re-uploads all three, then lookup mode
-    sync_volume(h, T_DX, T_DX);
-    sync_volume(h, T_DY, T_DY);
-    sync_volume(h, T_DZ, T_DZ);
+    // setGradientTextures (kernel.cu:703-722): (re-)upload all three, then lookup mode
+    sync_volume_if_changed(h, T_DX, T_DX);
+    sync_volume_if_changed(h, T_DY, T_DY);
+    sync_volume_if_changed(h, T_DZ, T_DZ);
     g_tex.grad_method = G_LOOKUP;
   }
-}
-
-bool env_flag(const char *name) {
-  const char *ev = std::getenv(name);
-  return ev && ev[0] == '1';
-}
-bool env_flag_off(const char *name) {
-  const char *ev = std::getenv(name);
-  return ev && ev[0] == '0';
 }
 
 vr::DevTex dev_tex(const BufPtr &b) {
@@ -567,7 +589,7 @@ void upload_lights(vr_context *h, const vr_render_args *a) {
   }
   if (n) VR_HIP(hipMemcpy(g_tex.d_lights, g_tex.lights.data(), n * sizeof(vr::DevLight), hipMemcpyHostToDevice));
   h->vol[T_LIGHT] = make_rec(a->illumination);
-  sync_volume(h, T_LIGHT, T_LIGHT);
+  sync_volume_if_changed(h, T_LIGHT, T_LIGHT);
 }
 
 int64_t part_columns(int64_t w, int32_t bc, int32_t part, int32_t np) {
