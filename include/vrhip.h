@@ -138,6 +138,33 @@ int64_t vr_partition_columns(int64_t w, const vr_partition *part);
 int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t block_cols,
                            int32_t num_parts, int64_t max_cols, float *d_out, void *stream);
 
+/* --- sort-last slabs (volumes larger than one GPU; no MATLAB counterpart: the
+ * reference aborts when a volume does not fit, mmanager.hxx:144-173) ----------------------------
+ * The handle's synced emission volume holds planes [z_first, z_first + d2) of a volume of depth
+ * `depth` (d0, d1 as synced).  The render marches every ray of the full W x H image over the
+ * samples it owns, those with z0 <= p.z * depth < z1 (p the normalized sample position; z0 = -inf
+ * / z1 = +inf for the end slabs), with positions, step counts and early exit exactly as the
+ * one-volume march.  Ray state: five planes of W*H floats, [c][x][y] = premultiplied r, g, b,
+ * alpha, and 1 if the ray continues past this slab; d_state_in NULL = fresh rays, may equal
+ * d_state_out.  direction +1 handles the rays with dir.z >= 0 (run the slabs in ascending z),
+ * -1 those with dir.z < 0 (descending); other rays pass through.  Chaining both sweeps over all
+ * slabs gives the one-volume image bit for bit in the first three planes.  Compute gradient or
+ * emission-absorption only; absorption must alias emission (the reference's default). */
+typedef struct vr_slab {
+  uint64_t depth;    /* global depth D of the emission volume                          */
+  uint64_t z_first;  /* global index of the first synced plane                         */
+  double z0, z1;     /* owned range of p.z * D                                         */
+  int32_t direction; /* +1 / -1                                                         */
+  int32_t reserved;
+} vr_slab;
+int vr_render_slab(vr_context *h, const vr_render_args *args, const vr_slab *slab, const float *d_state_in,
+                   float *d_state_out, void *stream);
+
+/* Planes [*first, *first + *count) of a volume of dims (d0, d1, D) a slab owning [z0, z1) must
+ * hold: the trilinear taps and the gradient taps of its samples (element size in MATLAB order). */
+int vr_slab_planes(const uint64_t dims[3], const float element_size_um[3], double z0, double z1, uint64_t *first,
+                   uint64_t *count);
+
 /* Depth lanes (lanes per ray) the march kernel uses for a launch of part_cols x
  * height rays on the current device: 1, 2, 4 or 8 (VR_DEPTH_LANES overrides).  Launches with few
  * waves per wave slot of the device also follow a longest-first workgroup schedule. */

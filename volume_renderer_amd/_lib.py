@@ -34,6 +34,11 @@ class VrRenderArgs(ctypes.Structure):
                 ("opacity_threshold", c_float), ("color", c_float * 3)]
 
 
+class VrSlab(ctypes.Structure):
+    _fields_ = [("depth", c_uint64), ("z_first", c_uint64), ("z0", ctypes.c_double), ("z1", ctypes.c_double),
+                ("direction", c_int32), ("reserved", c_int32)]
+
+
 class VrPartition(ctypes.Structure):
     _fields_ = [("block_cols", c_int32), ("part", c_int32), ("num_parts", c_int32),
                 ("reserved", c_int32)]
@@ -65,6 +70,9 @@ SIGNATURES = [
     ("vr_assemble_partitions", c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int64, c_void_p,
                                        c_void_p]),
     ("vr_depth_lanes", c_int, [c_int64, c_int64]),
+    ("vr_render_slab", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrSlab), c_void_p, c_void_p, c_void_p]),
+    ("vr_slab_planes", c_int, [POINTER(c_uint64), POINTER(c_float), ctypes.c_double, ctypes.c_double,
+                               POINTER(c_uint64), POINTER(c_uint64)]),
     ("vr_synth_shell_device", c_int, [c_void_p, c_uint64, c_void_p]),
     ("vr_gradient_device", c_int, [c_void_p, POINTER(c_uint64), c_void_p, c_void_p, c_void_p, c_void_p]),
     ("vr_debug_slot_transition", c_int, [POINTER(c_int32), c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,

@@ -38,6 +38,7 @@ hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool bi
   hipError_t launch_march_k2(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
   hipError_t launch_march_k4(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
   hipError_t launch_march_k8(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
+  hipError_t launch_march_slab(const RenderParams &, int, hipStream_t);                                   \
   uint32_t march_blocks_k1(const RenderParams &);                                                        \
   uint32_t march_blocks_k2(const RenderParams &);                                                        \
   uint32_t march_blocks_k4(const RenderParams &);                                                        \
@@ -447,7 +448,7 @@ struct Frame {
 };
 
 
-int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
+int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth_override = 0) {
   vr::RenderParams &P = F.P;
   std::memset(&P, 0, sizeof(P));
   const uint64_t H = a->resolution[0], W = a->resolution[1];
@@ -465,7 +466,7 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F) {
   // element size reversed (make_float3Inv, render.cpp:35-37,195)
   const float es[3] = {a->element_size_um[2], a->element_size_um[1], a->element_size_um[0]};
   const VolRec &ev = h->vol[T_EM];  // extent of the handle's emission volume (render.cpp:245)
-  const uint64_t vw = ev.dims[0], vh = ev.dims[1], vd = ev.dims[2];
+  const uint64_t vw = ev.dims[0], vh = ev.dims[1], vd = depth_override ? depth_override : ev.dims[2];
   float bmax[3];
   bmax[0] = 1.f;
   bmax[1] = (es[1] * (float)vh) / ((float)vw * es[0]);
@@ -804,6 +805,65 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   return VR_OK;
 }
 
+// Sort-last slab render: the handle's emission volume holds planes
+// [z_first, z_first + d2) of a volume of depth `depth`; the frame is built for the whole volume
+// (box, step, gradient offsets) and the march takes the samples of [z0, z1) only.
+int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, const float *d_in, float *d_out,
+                   hipStream_t stream, Frame &F) {
+  if (!sl || !d_out) return fail(VR_ERR_ARGUMENT, "slab / output is NULL");
+  const VolRec &ev = h->vol[T_EM];
+  if (sl->depth == 0 || sl->z_first + ev.dims[2] > sl->depth || (sl->direction != 1 && sl->direction != -1))
+    return fail(VR_ERR_ARGUMENT, "invalid slab");
+  if (a->num_lights > 0 && !a->lights) return fail(VR_ERR_ARGUMENT, "lights is NULL");
+  upload_lights(h, a);
+  int rc = build_frame(h, a, F, sl->depth);
+  if (rc) return rc;
+  vr::RenderParams &P = F.P;
+  if (F.degenerate || !P.em.p || P.em.one) return fail(VR_ERR_UNSUPPORTED, "slab render needs a synced emission volume");
+  if (F.mode == 2 || !F.ab_alias) return fail(VR_ERR_UNSUPPORTED, "slab render: lookup gradients / separate absorption");
+  // the resident planes addressed by their global padded index: virtual base z_first planes back
+  const bool re_em = P.re_is_em != 0;
+  P.em.p = P.em.p - (ptrdiff_t)(sl->z_first * (uint64_t)P.em.pxy);
+  P.em.nz = (int32_t)sl->depth;
+  P.em.fnz = (float)sl->depth;
+  P.gem = P.em;
+  if (re_em) P.re = P.em;
+  P.ab = P.em;
+  // resident padded planes holding the right data: the synced planes, plus the edge-replicating
+  // apron planes only at the ends of the whole volume
+  P.slab_pk0 = (int32_t)(sl->z_first + (sl->z_first > 0 ? 1 : 0));
+  P.slab_pk1 = (int32_t)(sl->z_first + ev.dims[2] + 1 + (sl->z_first + ev.dims[2] == sl->depth ? 1 : 0));
+  const double D = (double)sl->depth;
+  P.slab_z0 = std::isfinite(sl->z0) ? (float)(sl->z0 / D) : -INFINITY;
+  P.slab_z1 = std::isfinite(sl->z1) ? (float)(sl->z1 / D) : INFINITY;
+  // the z halo of build_frame was sized by the resident depth: redo it for the whole volume
+  {
+    double pmax = 0.0;
+    for (int i = 0; i < 3; ++i) pmax = std::max(pmax, (double)std::fabs(P.bmin[i]) + std::fabs(P.eye[i]));
+    F.drift1[2] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[2] * D;
+    P.tap_off[2] = (float)((F.mode == 1 ? (double)P.gstep[2] * P.bscale[2] * D : 0.0) + 0.0625);
+  }
+  set_chunk_halo(F, 1);
+  P.slab_margin = P.tap_off[2] / P.em.fnz;  // bound of the chunk ownership test, normalized
+  P.slab_dir = sl->direction;
+  P.slab_in = d_in;
+  P.block_cols = std::max<int32_t>(P.width, 1);
+  P.part = 0;
+  P.num_parts = 1;
+  P.part_cols = P.width;
+  P.plane_cols = P.width;
+  P.out = d_out;
+  P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
+  {
+    const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
+    const double tau = (f > 0 && P.width > 0) ? dist * (double)ev.dims[0] / ((double)P.width * f) : 1e30;
+    P.wide_slot = tau > 1.5 ? 1 : 0;
+  }
+  if (P.fast_shade) VR_HIP(vr::fast::launch_march_slab(P, F.mode, stream));
+  else VR_HIP(vr::exact::launch_march_slab(P, F.mode, stream));
+  return VR_OK;
+}
+
 #define VR_GUARD_BEGIN try {
 #define VR_GUARD_END                                                                             \
   }                                                                                              \
@@ -985,6 +1045,35 @@ int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t b
   VR_HIP(vr::launch_assemble(d_parts, w, h, block_cols, num_parts, max_cols, d_out, (hipStream_t)stream));
   return VR_OK;
   VR_GUARD_END
+}
+
+int vr_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *slab, const float *d_state_in,
+                   float *d_state_out, void *stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  Frame F;
+  return do_render_slab(h, a, slab, d_state_in, d_state_out, (hipStream_t)stream, F);
+  VR_GUARD_END
+}
+
+int vr_slab_planes(const uint64_t dims[3], const float element_size_um[3], double z0, double z1, uint64_t *first,
+                   uint64_t *count) {
+  if (!dims || !element_size_um || !first || !count || dims[0] == 0 || dims[2] == 0)
+    return fail(VR_ERR_ARGUMENT, "invalid slab geometry");
+  // gradient tap offset along z in texels (volumeRender.cpp:273-275 through initRender's box):
+  // gstep_z * bscale_z * D = vw * es_x / (2 * es_z * D), es reversed as render.cpp:195 does
+  const double esx = element_size_um[2], esz = element_size_um[0];
+  const double D = (double)dims[2];
+  const double off = (double)dims[0] * esx / (2.0 * esz * D) + 0.5;
+  const double lo = std::isfinite(z0) ? std::floor(z0 - 0.5 - off) - 1.0 : 0.0;
+  const double hi = std::isfinite(z1) ? std::floor(z1 - 0.5 + off) + 3.0 : D;
+  const double a = std::min(std::max(lo, 0.0), D), b = std::min(std::max(hi, 0.0), D);
+  *first = (uint64_t)a;
+  *count = b > a ? (uint64_t)(b - a) : 0;
+  return VR_OK;
 }
 
 int vr_depth_lanes(int64_t part_cols, int64_t height) {

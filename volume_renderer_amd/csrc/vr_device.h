@@ -71,6 +71,12 @@ struct RenderParams {
   uint32_t prio_blocks;           // scheduled launch: the first prio_blocks workgroups (the longest)
                                   // run at raised wave priority
   unsigned long long *steps;      // optional sample counter
+  // sort-last slab launch (vr_render_slab): owned normalized z range [slab_z0,
+  // slab_z1), the margin of the chunk ownership test, the resident padded planes [slab_pk0,
+  // slab_pk1) of the emission texture, the sweep direction, the incoming ray state (or null)
+  float slab_z0, slab_z1, slab_margin;
+  int32_t slab_pk0, slab_pk1, slab_dir;
+  const float *slab_in;
 };
 
 // Per-buffer statistics computed on the device at upload (used to prove the empty-sample skip

@@ -83,6 +83,7 @@ struct Ray {
   int32_t nsteps, nlit;
   bool alive;
   bool mine;  // K > 1: this lane's current sample exists (see march)
+  bool past;  // slab mode: the ray left this rank's slab still unfinished (the next slab goes on)
 };
 
 struct ChunkStats {
@@ -223,9 +224,19 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, i
 // takes its sample, then every lane composites the group's samples in order; `alive` (the ray:
 // not stopped by sum.a > thr and some sample left) is the same in all K lanes.  Bit-identical to
 // K = 1; samples after an early exit are computed and discarded.
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP>
+// SLAB (sort-last bricks; K = 1 only): the emission texture holds planes of one
+// z-slab of a larger volume, and only the samples this slab owns (slab_z0 <= p.z < slab_z1 in
+// normalized coordinates) are fetched and composited; the others replay the march recurrences
+// only, so every owned sample has the position, t and step count of the one-volume march.  A ray
+// stops here when it leaves the slab in its direction of travel (`past`), or terminates.
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
   static_assert(!COUNT || K == 1, "the counter variant is built for K = 1 only");
+  static_assert(!SLAB || (K == 1 && !COUNT && BIG), "slab mode: K = 1, 64-bit addressing");
+  const float sbz = P.bmin[2], ssz = P.bscale[2];
+  const bool asc = R.step.z >= 0.f;  // slab order along this ray
+  // slab mode: the ray has left the slab in its direction of travel (normalized z of its sample)
+  auto beyond = [&](float zn) { return asc ? zn >= P.slab_z1 : zn < P.slab_z0; };
   const DevTex &E = P.em;
   const int sub = lane & (K - 1);
   if constexpr (K > 1) {
@@ -243,6 +254,34 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     int box_vol = 0;
     plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B,
                     COUNT ? &box_vol : nullptr);
+    if constexpr (SLAB) {
+      // a chunk none of whose samples this slab owns only replays the recurrences
+      bool own = false;
+      if (R.alive) {
+        const float zs = (R.pos.z - sbz) * ssz;
+        const float ze = (fmaf(R.step.z, (float)(S - 1), R.pos.z) - sbz) * ssz;
+        own = fmaxf(zs, ze) + P.slab_margin >= P.slab_z0 && fminf(zs, ze) - P.slab_margin < P.slab_z1;
+      }
+      if (!__any(own)) {
+        advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        if (R.alive && beyond((R.pos.z - sbz) * ssz)) {
+          R.alive = false;
+          R.past = true;
+        }
+        continue;
+      }
+      // only this slab's planes are resident: clamp the staged box to them (the owned samples'
+      // taps lie inside; the others are not fetched)
+      const int z_lo = max(B.rz, P.slab_pk0), z_hi = min(B.rz + B.ez, P.slab_pk1);
+      if (staged) {
+        if (z_hi <= z_lo) {
+          staged = false;
+        } else {
+          B.rz = z_lo;
+          B.ez = z_hi - z_lo;
+        }
+      }
+    }
     if (COUNT && lane == 0) {  // diagnostics: box volume of partial/failed chunks, S of staged ones
       if (!staged || partial) atomicAdd(P.steps + 8 + min(box_vol >> 8, 31), 1ull);
       else atomicAdd(P.steps + 40 + (S >= 32 ? 0 : (S >= 16 ? 1 : (S >= 8 ? 2 : 3))), 1ull);
@@ -271,6 +310,25 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     // ---- S samples ---------------------------------------------------------------------------
     if constexpr (K == 1) {
       for (int k = 0; k < S && R.alive; ++k) {
+        if constexpr (SLAB) {
+          const float zn = (R.pos.z - sbz) * ssz;  // the sampler's own p.z
+          if (!(zn >= P.slab_z0 && zn < P.slab_z1)) {
+            if (beyond(zn)) {
+              R.alive = false;
+              R.past = true;
+            } else {  // before the slab: the recurrences of one sample (composite without colour)
+              ++R.nsteps;
+              if (R.nsteps >= P.max_steps) {
+                R.alive = false;
+              } else {
+                R.t += P.tstep;
+                if (R.t > R.tfar) R.alive = false;
+                else R.pos = mk(R.pos.x + R.step.x, R.pos.y + R.step.y, R.pos.z + R.step.z);
+              }
+            }
+            continue;
+          }
+        }
         float r, gg, b, alpha;
         bool shaded;
         sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
@@ -403,6 +461,88 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     }
   }
 }
+
+#if VR_MARCH_K == 1
+// Sort-last slab launch: one wave per 8x8 tile of the full image; per pixel the ray
+// state (premultiplied r, g, b, alpha, and 1 if the ray goes on past this slab) is read from
+// P.slab_in (null: a fresh ray), marched through this slab's samples and written to P.out as five
+// [W][H] planes.  Rays whose direction does not match the sweep (P.slab_dir: +1 = rays with
+// dir.z >= 0 in ascending slab order, -1 = dir.z < 0 descending) pass their state through.
+template <int MODE, int CAP>
+__global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const RenderParams P) {
+  __shared__ float lds[VR_WG_WAVES][CAP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float *L = lds[wave];
+  const int tile = (int)blockIdx.x * VR_WG_WAVES + wave;
+  const int nbx = (P.width + 15) >> 4;
+  const int blk = tile >> 2, quad = tile & 3;
+  const int x = (blk % nbx) * 16 + (quad & 1) * 8 + (lane >> 3);
+  const int y = (blk / nbx) * 16 + (quad >> 1) * 8 + (lane & 7);
+  const bool active = (x < P.width) && (y < P.height);
+  const size_t plane = (size_t)P.width * (size_t)P.height;
+  const size_t kk = (size_t)x * (size_t)P.height + (size_t)y;
+  Ray R;
+  R.o = mk(0.f, 0.f, 0.f);
+  R.pos = R.o;
+  R.step = R.o;
+  R.t = 0.f;
+  R.tfar = -1.f;
+  R.sr = R.sg = R.sb = R.sa = 0.f;
+  R.nsteps = R.nlit = 0;
+  R.alive = false;
+  R.mine = false;
+  R.past = false;
+  bool go_on = true;  // the incoming state: the ray has not terminated
+  ChunkStats C{0, 0, 0, 0, 0};
+  if (active) {
+    if (P.slab_in) {
+      R.sr = P.slab_in[kk];
+      R.sg = P.slab_in[kk + plane];
+      R.sb = P.slab_in[kk + 2 * plane];
+      R.sa = P.slab_in[kk + 3 * plane];
+      go_on = P.slab_in[kk + 4 * plane] != 0.f;
+    }
+    f3 d;
+    float tnear;
+    const bool hit = ray_setup(P, x, y, R.o, d, tnear, R.tfar);
+    R.pos = mk(fmaf(d.x, tnear, R.o.x), fmaf(d.y, tnear, R.o.y), fmaf(d.z, tnear, R.o.z));
+    R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
+    R.t = tnear;
+    const bool mine_dir = (P.slab_dir > 0) == (R.step.z >= 0.f);
+    R.alive = hit && go_on && mine_dir;
+    R.past = go_on && !mine_dir;  // another sweep's ray: passed through unchanged
+    if (!hit) R.past = false;
+  }
+  if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+    march<1, MODE, true, false, false, true, false, CAP, true>(P, L, lane, R, C);
+  else
+    march<1, MODE, true, false, false, true, true, CAP, true>(P, L, lane, R, C);
+  if (active) {
+    P.out[kk] = R.sr;
+    P.out[kk + plane] = R.sg;
+    P.out[kk + 2 * plane] = R.sb;
+    P.out[kk + 3 * plane] = R.sa;
+    P.out[kk + 4 * plane] = R.past ? 1.f : 0.f;
+  }
+}
+
+// Host entry of the slab launch (built in the K = 1 object): MODE 0 or 1, absorption aliasing
+// emission, the emission texture addressed with 64-bit offsets from its virtual base.
+hipError_t launch_march_slab(const RenderParams &P, int mode, hipStream_t s) {
+  if (P.width <= 0 || P.height <= 0) return hipSuccess;
+  if (mode > 1) return hipErrorInvalidValue;
+  const uint64_t tiles = (uint64_t)((P.width + 15) / 16) * (uint64_t)((P.height + 15) / 16) * 4;
+  const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES)), blk(64 * VR_WG_WAVES);
+  if (mode == 0) {
+    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<0, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_slab_kernel<0, VR_LDS_CAP>), grid, blk, 0, s, P);
+  } else {
+    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<1, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_slab_kernel<1, VR_LDS_CAP>), grid, blk, 0, s, P);
+  }
+  return hipGetLastError();
+}
+#endif
 
 template <int MODE, bool AB, bool SH, int CAP>
 static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {

@@ -175,6 +175,30 @@ def partition_columns(width: int, part) -> int:
     return int(lib().vr_partition_columns(int(width), ctypes.byref(part) if part is not None else None))
 
 
+def slab(depth: int, z_first: int, z0: float, z1: float, direction: int) -> _lib.VrSlab:
+    """vr_slab: the synced emission volume holds planes [z_first, ...) of a volume of depth
+    `depth`; the render owns the samples with z0 <= p.z * depth < z1; direction +1 / -1."""
+    s = _lib.VrSlab()
+    s.depth, s.z_first, s.z0, s.z1, s.direction = int(depth), int(z_first), float(z0), float(z1), int(direction)
+    return s
+
+
+def slab_planes(dims, element_size_um, z0: float, z1: float):
+    """(first, count): the planes a slab owning [z0, z1) of a (d0, d1, D) volume must hold."""
+    d = (ctypes.c_uint64 * 3)(*[int(x) for x in dims])
+    es = (ctypes.c_float * 3)(*[float(x) for x in element_size_um])
+    first, count = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(lib().vr_slab_planes(d, es, float(z0), float(z1), ctypes.byref(first), ctypes.byref(count)))
+    return int(first.value), int(count.value)
+
+
+def render_slab(handle, ra: VrRenderArgs, sl, d_state_in: int, d_state_out: int, stream: int = 0) -> None:
+    """vr_render_slab: march this slab's samples of every ray; state = 5 planes of W*H floats."""
+    check(lib().vr_render_slab(_handle(handle), ctypes.byref(ra), ctypes.byref(sl),
+                               ctypes.c_void_p(int(d_state_in)) if d_state_in else None,
+                               ctypes.c_void_p(int(d_state_out)), ctypes.c_void_p(int(stream))))
+
+
 def depth_lanes(part_cols: int, height: int) -> int:
     """Depth lanes the march uses for a launch of this shape on the current device (vr_depth_lanes)."""
     return int(lib().vr_depth_lanes(int(part_cols), int(height)))
