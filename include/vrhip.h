@@ -144,8 +144,10 @@ int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t b
  * `depth` (d0, d1 as synced).  The render marches every ray of the full W x H image over the
  * samples it owns, those with z0 <= p.z * depth < z1 (p the normalized sample position; z0 = -inf
  * / z1 = +inf for the end slabs), with positions, step counts and early exit exactly as the
- * one-volume march.  Ray state: five planes of W*H floats, [c][x][y] = premultiplied r, g, b,
- * alpha, and 1 if the ray continues past this slab; d_state_in NULL = fresh rays, may equal
+ * one-volume march.  part (NULL = the whole image) restricts the render to the columns of an
+ * image partition (the tiles of a pipelined multi-GPU sweep).  Ray state: five planes of
+ * cols*H floats, [c][local column][y] = premultiplied r, g, b, alpha, and 1 if the ray continues
+ * past this slab (cols = vr_partition_columns); d_state_in NULL = fresh rays, may equal
  * d_state_out.  direction +1 handles the rays with dir.z >= 0 (run the slabs in ascending z),
  * -1 those with dir.z < 0 (descending); other rays pass through.  Chaining both sweeps over all
  * slabs gives the one-volume image bit for bit in the first three planes.  Compute gradient or
@@ -157,8 +159,8 @@ typedef struct vr_slab {
   int32_t direction; /* +1 / -1                                                         */
   int32_t reserved;
 } vr_slab;
-int vr_render_slab(vr_context *h, const vr_render_args *args, const vr_slab *slab, const float *d_state_in,
-                   float *d_state_out, void *stream);
+int vr_render_slab(vr_context *h, const vr_render_args *args, const vr_slab *slab, const vr_partition *part,
+                   const float *d_state_in, float *d_state_out, void *stream);
 
 /* Planes [*first, *first + *count) of a volume of dims (d0, d1, D) a slab owning [z0, z1) must
  * hold: the trilinear taps and the gradient taps of its samples (element size in MATLAB order). */
@@ -172,6 +174,9 @@ int vr_depth_lanes(int64_t part_cols, int64_t height);
 
 /* Synthetic test volume V_shell(n) of SURVEY.md 8d, generated on the device into d_out[n^3]. */
 int vr_synth_shell_device(float *d_out, uint64_t n, void *stream);
+
+/* Planes [z_first, z_first + count) of V_shell(n) into d_out[n*n*count] (a sort-last slab's share). */
+int vr_synth_shell_planes_device(float *d_out, uint64_t n, uint64_t z_first, uint64_t count, void *stream);
 
 /* Volume.grad on the device (Volume.m:181-205, MATLAB gradient() of single data): for the
  * column-major d_data[d0*d1*d2] writes d_gx (along dim 2), d_gy (along dim 1), d_gz (along dim 3),

@@ -453,13 +453,16 @@ def _slab_chain(data, es, bounds, lights, lut, ra_args, W, H, shade):
     return np.ascontiguousarray(np.transpose(st[:3], (2, 1, 0))), st  # [H, W, 3]
 
 
+@pytest.mark.parametrize("lanes", ["1", "2", "4"])
 @pytest.mark.parametrize("shade", ["fast", "exact"])
 @pytest.mark.parametrize("case", ["cube3", "aniso4"])
-def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case, shade):
+def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case, shade, lanes):
     """Sort-last bricks: a volume split into z-slabs, each rendered with only
     its own planes resident, composited by passing the exact ray state from slab to slab in ray
     order (ascending z for rays with dir.z >= 0, descending for the others) gives the one-volume
-    image bit for bit -- same sample positions, step counts and early exits."""
+    image bit for bit -- same sample positions, step counts and early exits -- with any depth
+    lanes in the slab launches."""
+    monkeypatch.setenv("VR_DEPTH_LANES", lanes)
     if shade == "exact":
         monkeypatch.setenv("VR_EXACT_SHADE", "1")
     else:
@@ -474,7 +477,9 @@ def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case
     v = vr.Volume(data)
     r = ex1_renderer(v, res=(W, H))
     r.ElementSizeUm = es
+    monkeypatch.delenv("VR_DEPTH_LANES")
     full = r.render()
+    monkeypatch.setenv("VR_DEPTH_LANES", lanes)
     lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
     ra_args = (np.float32([1.0, 0.4, 0.6]), np.float32(es), np.uint64([H, W]),
                np.flip(r.RotationMatrix, 0).astype(np.float32), np.float32([0, 3.0, 6.0]), np.float32(0.9),

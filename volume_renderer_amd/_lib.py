@@ -70,10 +70,12 @@ SIGNATURES = [
     ("vr_assemble_partitions", c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int64, c_void_p,
                                        c_void_p]),
     ("vr_depth_lanes", c_int, [c_int64, c_int64]),
-    ("vr_render_slab", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrSlab), c_void_p, c_void_p, c_void_p]),
+    ("vr_render_slab", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrSlab), POINTER(VrPartition), c_void_p,
+                                c_void_p, c_void_p]),
     ("vr_slab_planes", c_int, [POINTER(c_uint64), POINTER(c_float), ctypes.c_double, ctypes.c_double,
                                POINTER(c_uint64), POINTER(c_uint64)]),
     ("vr_synth_shell_device", c_int, [c_void_p, c_uint64, c_void_p]),
+    ("vr_synth_shell_planes_device", c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
     ("vr_gradient_device", c_int, [c_void_p, POINTER(c_uint64), c_void_p, c_void_p, c_void_p, c_void_p]),
     ("vr_debug_slot_transition", c_int, [POINTER(c_int32), c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                          POINTER(c_int32), POINTER(c_int32)]),

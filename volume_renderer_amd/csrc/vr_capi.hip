@@ -38,7 +38,9 @@ hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool bi
   hipError_t launch_march_k2(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
   hipError_t launch_march_k4(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
   hipError_t launch_march_k8(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
-  hipError_t launch_march_slab(const RenderParams &, int, hipStream_t);                                   \
+  hipError_t launch_march_slab_k1(const RenderParams &, int, hipStream_t);                                \
+  hipError_t launch_march_slab_k2(const RenderParams &, int, hipStream_t);                                \
+  hipError_t launch_march_slab_k4(const RenderParams &, int, hipStream_t);                                \
   uint32_t march_blocks_k1(const RenderParams &);                                                        \
   uint32_t march_blocks_k2(const RenderParams &);                                                        \
   uint32_t march_blocks_k4(const RenderParams &);                                                        \
@@ -54,7 +56,7 @@ hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t 
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
-hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s);
+hipError_t launch_synth_shell(float *out, uint64_t n, uint64_t z_first, uint64_t nz, hipStream_t s);
 hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, float *gy, float *gz, hipStream_t s);
 }  // namespace vr
 
@@ -808,8 +810,8 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
 // Sort-last slab render: the handle's emission volume holds planes
 // [z_first, z_first + d2) of a volume of depth `depth`; the frame is built for the whole volume
 // (box, step, gradient offsets) and the march takes the samples of [z0, z1) only.
-int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, const float *d_in, float *d_out,
-                   hipStream_t stream, Frame &F) {
+int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, const vr_partition *part,
+                   const float *d_in, float *d_out, hipStream_t stream, Frame &F) {
   if (!sl || !d_out) return fail(VR_ERR_ARGUMENT, "slab / output is NULL");
   const VolRec &ev = h->vol[T_EM];
   if (sl->depth == 0 || sl->z_first + ev.dims[2] > sl->depth || (sl->direction != 1 && sl->direction != -1))
@@ -843,15 +845,17 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
     F.drift1[2] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[2] * D;
     P.tap_off[2] = (float)((F.mode == 1 ? (double)P.gstep[2] * P.bscale[2] * D : 0.0) + 0.0625);
   }
-  set_chunk_halo(F, 1);
+  set_chunk_halo(F, 4);  // the slab launch marches with up to 4 depth lanes (chunks <= 64 samples)
   P.slab_margin = P.tap_off[2] / P.em.fnz;  // bound of the chunk ownership test, normalized
   P.slab_dir = sl->direction;
   P.slab_in = d_in;
-  P.block_cols = std::max<int32_t>(P.width, 1);
-  P.part = 0;
-  P.num_parts = 1;
-  P.part_cols = P.width;
-  P.plane_cols = P.width;
+  rc = validate_partition(part);
+  if (rc) return rc;
+  P.block_cols = part ? part->block_cols : std::max<int32_t>(P.width, 1);
+  P.part = part ? part->part : 0;
+  P.num_parts = part ? part->num_parts : 1;
+  P.part_cols = (int32_t)part_columns(P.width, P.block_cols, P.part, P.num_parts);
+  P.plane_cols = P.part_cols;  // the state of a part is dense: five [part_cols][H] planes
   P.out = d_out;
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
   {
@@ -859,8 +863,14 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
     const double tau = (f > 0 && P.width > 0) ? dist * (double)ev.dims[0] / ((double)P.width * f) : 1e30;
     P.wide_slot = tau > 1.5 ? 1 : 0;
   }
-  if (P.fast_shade) VR_HIP(vr::fast::launch_march_slab(P, F.mode, stream));
-  else VR_HIP(vr::exact::launch_march_slab(P, F.mode, stream));
+  // depth lanes as for the one-volume march (a tile of a pipelined sweep is a short launch)
+  int K = depth_lanes(P);
+  if (K > 4) K = 4;
+  typedef hipError_t (*slab_fn)(const vr::RenderParams &, int, hipStream_t);
+  static const slab_fn sfns[2][3] = {
+      {vr::exact::launch_march_slab_k1, vr::exact::launch_march_slab_k2, vr::exact::launch_march_slab_k4},
+      {vr::fast::launch_march_slab_k1, vr::fast::launch_march_slab_k2, vr::fast::launch_march_slab_k4}};
+  VR_HIP(sfns[P.fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](P, F.mode, stream));
   return VR_OK;
 }
 
@@ -1047,15 +1057,15 @@ int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t b
   VR_GUARD_END
 }
 
-int vr_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *slab, const float *d_state_in,
-                   float *d_state_out, void *stream) {
+int vr_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *slab, const vr_partition *part,
+                   const float *d_state_in, float *d_state_out, void *stream) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
   if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
   Frame F;
-  return do_render_slab(h, a, slab, d_state_in, d_state_out, (hipStream_t)stream, F);
+  return do_render_slab(h, a, slab, part, d_state_in, d_state_out, (hipStream_t)stream, F);
   VR_GUARD_END
 }
 
@@ -1086,7 +1096,15 @@ int vr_depth_lanes(int64_t part_cols, int64_t height) {
 
 int vr_synth_shell_device(float *d_out, uint64_t n, void *stream) {
   VR_GUARD_BEGIN
-  VR_HIP(vr::launch_synth_shell(d_out, n, (hipStream_t)stream));
+  VR_HIP(vr::launch_synth_shell(d_out, n, 0, n, (hipStream_t)stream));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_synth_shell_planes_device(float *d_out, uint64_t n, uint64_t z_first, uint64_t count, void *stream) {
+  if (z_first + count > n) return fail(VR_ERR_ARGUMENT, "planes outside the volume");
+  VR_GUARD_BEGIN
+  VR_HIP(vr::launch_synth_shell(d_out, n, z_first, count, (hipStream_t)stream));
   return VR_OK;
   VR_GUARD_END
 }

@@ -173,12 +173,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(const float *__restrict__
 // V_shell(n), SURVEY.md 8d: normalized voxel centres x=(i+.5)/n ..., r = |(x,y,z) - .5|,
 // v = clamp(1 - |r - .32|/.14, 0, 1) * (.6 + .4 sin(6 pi x) sin(6 pi y) sin(6 pi z))
 //     + .05 (x + 2y + 3z)/6 [v > 0]
-__global__ __launch_bounds__(256) void synth_shell_kernel(float *__restrict__ out, uint64_t n) {
-  const uint64_t total = n * n * n;
+__global__ __launch_bounds__(256) void synth_shell_kernel(float *__restrict__ out, uint64_t n, uint64_t z_first,
+                                                          uint64_t nz) {
+  const uint64_t total = n * n * nz;
   const double inv = 1.0 / (double)n;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t a = i % n, bq = i / n, b = bq % n, c = bq / n;
+    const uint64_t a = i % n, bq = i / n, b = bq % n, c = bq / n + z_first;
     const double x = (a + 0.5) * inv, y = (b + 0.5) * inv, z = (c + 0.5) * inv;
     const double dx = x - 0.5, dy = y - 0.5, dz = z - 0.5;
     const double r = sqrt(dx * dx + dy * dy + dz * dz);
@@ -393,12 +394,12 @@ hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_synth_shell(float *out, uint64_t n, hipStream_t s) {
-  const uint64_t total = n * n * n;
+hipError_t launch_synth_shell(float *out, uint64_t n, uint64_t z_first, uint64_t nz, hipStream_t s) {
+  const uint64_t total = n * n * nz;
   if (!total) return hipSuccess;
   uint64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(synth_shell_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, n);
+  hipLaunchKernelGGL(synth_shell_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, n, z_first, nz);
   return hipGetLastError();
 }
 

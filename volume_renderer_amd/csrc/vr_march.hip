@@ -232,7 +232,7 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, i
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
   static_assert(!COUNT || K == 1, "the counter variant is built for K = 1 only");
-  static_assert(!SLAB || (K == 1 && !COUNT && BIG), "slab mode: K = 1, 64-bit addressing");
+  static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
   const float sbz = P.bmin[2], ssz = P.bscale[2];
   const bool asc = R.step.z >= 0.f;  // slab order along this ray
   // slab mode: the ray has left the slab in its direction of travel (normalized z of its sample)
@@ -263,10 +263,21 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         own = fmaxf(zs, ze) + P.slab_margin >= P.slab_z0 && fminf(zs, ze) - P.slab_margin < P.slab_z1;
       }
       if (!__any(own)) {
-        advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
-        if (R.alive && beyond((R.pos.z - sbz) * ssz)) {
-          R.alive = false;
-          R.past = true;
+        if constexpr (K == 1) {
+          advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
+          if (R.alive && beyond((R.pos.z - sbz) * ssz)) {
+            R.alive = false;
+            R.past = true;
+          }
+        } else {
+          advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+          R.alive = R.alive && group_any<K>(R.mine);
+          // the ray's next sample is lane 0's
+          const bool b0 = group_lane<K, 0>(beyond((R.pos.z - sbz) * ssz) ? 1.f : 0.f) != 0.f;
+          if (R.alive && b0) {
+            R.alive = false;
+            R.past = true;
+          }
         }
         continue;
       }
@@ -342,13 +353,28 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     } else {
       for (int k = 0; k < S && R.alive; k += K) {
         float r = 0.f, gg = 0.f, b = 0.f, alpha = 0.f;
-        if (R.mine) {
+        bool ex = R.mine, take = R.mine;
+        if constexpr (SLAB) {
+          // a sample beyond the slab ends the ray here (beyond is monotone along the ray, so the
+          // group's existing samples stay a prefix); one before it adds exactly nothing (colour 0,
+          // opacity 0: the sums and the exit test are unchanged)
+          const float zn = (R.pos.z - sbz) * ssz;
+          if (ex && beyond(zn)) ex = false;
+          take = ex && zn >= P.slab_z0 && zn < P.slab_z1;
+        }
+        if (take) {
           bool shaded;
           sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
         }
-        const uint64_t m = __ballot(R.mine);
+        const uint64_t m = __ballot(ex);
         const int nv = __popcll((m >> (lane & ~(K - 1))) & ((1ull << K) - 1));  // existing samples
         composite_group<K, 0>(P, R, nv, r, gg, b, alpha);
+        if constexpr (SLAB) {
+          if (R.alive && group_any<K>(R.mine && !ex)) {  // left the slab still unfinished
+            R.alive = false;
+            R.past = true;
+          }
+        }
         advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to sample + K
         R.alive = R.alive && group_any<K>(R.mine);
       }
@@ -462,25 +488,29 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   }
 }
 
-#if VR_MARCH_K == 1
-// Sort-last slab launch: one wave per 8x8 tile of the full image; per pixel the ray
-// state (premultiplied r, g, b, alpha, and 1 if the ray goes on past this slab) is read from
-// P.slab_in (null: a fresh ray), marched through this slab's samples and written to P.out as five
-// [W][H] planes.  Rays whose direction does not match the sweep (P.slab_dir: +1 = rays with
+#if VR_MARCH_K <= 4
+// Sort-last slab launch: one wave per 8x8 tile of the image part (the columns of
+// the image partition, vr_partition); per pixel the ray state (premultiplied r, g, b, alpha, and
+// 1 if the ray goes on past this slab) is read from P.slab_in (null: a fresh ray), marched
+// through this slab's samples and written to P.out as five [plane_cols][H] planes.  Rays whose direction does not match the sweep (P.slab_dir: +1 = rays with
 // dir.z >= 0 in ascending slab order, -1 = dir.z < 0 descending) pass their state through.
-template <int MODE, int CAP>
+template <int K, int MODE, int CAP>
 __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const RenderParams P) {
+  using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
   const int tile = (int)blockIdx.x * VR_WG_WAVES + wave;
-  const int nbx = (P.width + 15) >> 4;
+  const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
   const int blk = tile >> 2, quad = tile & 3;
-  const int x = (blk % nbx) * 16 + (quad & 1) * 8 + (lane >> 3);
-  const int y = (blk / nbx) * 16 + (quad >> 1) * 8 + (lane & 7);
-  const bool active = (x < P.width) && (y < P.height);
-  const size_t plane = (size_t)P.width * (size_t)P.height;
-  const size_t kk = (size_t)x * (size_t)P.height + (size_t)y;
+  const int ray = lane >> TS::LK;
+  const int lc = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + (ray / TS::TH);  // local column
+  const int y = (blk / nbx) * (2 * TS::TH) + (quad >> 1) * TS::TH + (ray % TS::TH);
+  const bool active = (lc < P.part_cols) && (y < P.height);
+  const int pb = lc / P.block_cols;
+  const int x = (P.part + pb * P.num_parts) * P.block_cols + (lc - pb * P.block_cols);
+  const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
+  const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
   Ray R;
   R.o = mk(0.f, 0.f, 0.f);
   R.pos = R.o;
@@ -514,10 +544,10 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const Rend
     if (!hit) R.past = false;
   }
   if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<1, MODE, true, false, false, true, false, CAP, true>(P, L, lane, R, C);
+    march<K, MODE, true, false, false, true, false, CAP, true>(P, L, lane, R, C);
   else
-    march<1, MODE, true, false, false, true, true, CAP, true>(P, L, lane, R, C);
-  if (active) {
+    march<K, MODE, true, false, false, true, true, CAP, true>(P, L, lane, R, C);
+  if (active && (lane & (K - 1)) == 0) {
     P.out[kk] = R.sr;
     P.out[kk + plane] = R.sg;
     P.out[kk + 2 * plane] = R.sb;
@@ -526,19 +556,22 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const Rend
   }
 }
 
-// Host entry of the slab launch (built in the K = 1 object): MODE 0 or 1, absorption aliasing
-// emission, the emission texture addressed with 64-bit offsets from its virtual base.
-hipError_t launch_march_slab(const RenderParams &P, int mode, hipStream_t s) {
-  if (P.width <= 0 || P.height <= 0) return hipSuccess;
+// Host entry of the slab launch (launch_march_slab_k1 / _k2 / _k4): MODE 0 or 1, absorption
+// aliasing emission, the emission texture addressed with 64-bit offsets from its virtual base.
+hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mode, hipStream_t s) {
+  constexpr int K = VR_MARCH_K;
+  using TS = TileShape<K>;
+  if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
   if (mode > 1) return hipErrorInvalidValue;
-  const uint64_t tiles = (uint64_t)((P.width + 15) / 16) * (uint64_t)((P.height + 15) / 16) * 4;
+  const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
+                         (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES)), blk(64 * VR_WG_WAVES);
   if (mode == 0) {
-    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<0, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_slab_kernel<0, VR_LDS_CAP>), grid, blk, 0, s, P);
+    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<K, 0, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_slab_kernel<K, 0, VR_LDS_CAP>), grid, blk, 0, s, P);
   } else {
-    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<1, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_slab_kernel<1, VR_LDS_CAP>), grid, blk, 0, s, P);
+    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<K, 1, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_slab_kernel<K, 1, VR_LDS_CAP>), grid, blk, 0, s, P);
   }
   return hipGetLastError();
 }

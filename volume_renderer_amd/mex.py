@@ -192,9 +192,12 @@ def slab_planes(dims, element_size_um, z0: float, z1: float):
     return int(first.value), int(count.value)
 
 
-def render_slab(handle, ra: VrRenderArgs, sl, d_state_in: int, d_state_out: int, stream: int = 0) -> None:
-    """vr_render_slab: march this slab's samples of every ray; state = 5 planes of W*H floats."""
+def render_slab(handle, ra: VrRenderArgs, sl, d_state_in: int, d_state_out: int, stream: int = 0,
+                part=None) -> None:
+    """vr_render_slab: march this slab's samples of every ray (of the part's columns, if a
+    partition is given); state = 5 planes of cols*H floats."""
     check(lib().vr_render_slab(_handle(handle), ctypes.byref(ra), ctypes.byref(sl),
+                               ctypes.byref(part) if part is not None else None,
                                ctypes.c_void_p(int(d_state_in)) if d_state_in else None,
                                ctypes.c_void_p(int(d_state_out)), ctypes.c_void_p(int(stream))))
 
@@ -221,6 +224,11 @@ def assemble_partitions(d_parts: int, width: int, height: int, block_cols: int, 
 def synth_shell_device(d_out: int, n: int, stream: int = 0) -> None:
     check(lib().vr_synth_shell_device(ctypes.c_void_p(int(d_out)), int(n),
                                       ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def synth_shell_planes_device(d_out: int, n: int, z_first: int, count: int, stream: int = 0) -> None:
+    check(lib().vr_synth_shell_planes_device(ctypes.c_void_p(int(d_out)), int(n), int(z_first), int(count),
+                                             ctypes.c_void_p(int(stream))))
 
 
 def gradient_device(d_data: int, dims, d_gx: int, d_gy: int, d_gz: int, stream: int = 0) -> None:

@@ -36,3 +36,49 @@ def gather_partitions(local, gathered, world: int, rank: int, group=None) -> Non
             gathered.copy_(local)
         return
     dist.gather(local, list(gathered.chunk(world)) if rank == 0 else None, dst=0, group=group)
+
+
+# ---- sort-last z-slabs -----------------------------------------
+# Volumes larger than one GPU: rank r holds only the planes of z-slab r (vr_slab_planes) and
+# marches only the samples that slab owns (vr_render_slab).  A ray's samples are composited in ray
+# order by handing the exact ray state (premultiplied rgb, alpha, "goes on") from slab to slab:
+# rays with dir.z >= 0 visit the slabs in ascending z (rank 0 -> world-1), the others descending
+# (world-1 -> 0).  The image is cut into `ntiles` column tiles (vr_partition parts) so that the
+# ranks work on different tiles at the same time: rank r renders tile t of the ascending sweep once
+# rank r-1 has sent it, then the descending sweep runs back down; rank 0 ends with every ray's
+# final state, bit-identical to the one-volume render.
+
+def slab_bounds(depth: int, world: int):
+    """Owned ranges [z0, z1) of `world` equal z-slabs of a depth-`depth` volume (the end slabs
+    open towards -inf / +inf so that no sample is left without an owner)."""
+    cuts = [round(depth * r / world) for r in range(1, world)]
+    return [(-float("inf") if r == 0 else float(cuts[r - 1]), float("inf") if r == world - 1 else float(cuts[r]))
+            for r in range(world)]
+
+
+def sort_last_sweeps(render_tile, states, world: int, rank: int, group=None) -> None:
+    """Run the two pipelined sweeps.  `render_tile(t, direction, fresh, buf)` renders this rank's
+    slab for tile t in place on buf (fresh: the tile's rays start here, no incoming state);
+    `states[t]` is this rank's state buffer of tile t (a tensor the backend can send).  On return
+    rank 0's buffers hold the final state of every tile."""
+    import torch.distributed as dist
+    pending = []
+    # ascending sweep: rank 0 starts every tile fresh
+    for t, buf in enumerate(states):
+        if rank > 0:
+            dist.recv(buf, src=rank - 1, group=group)
+        render_tile(t, +1, rank == 0, buf)
+        if rank < world - 1:
+            pending.append(dist.isend(buf, dst=rank + 1, group=group))
+    for w in pending:
+        w.wait()
+    pending = []
+    # descending sweep: the last rank continues from its own ascending result
+    for t, buf in enumerate(states):
+        if rank < world - 1:
+            dist.recv(buf, src=rank + 1, group=group)
+        render_tile(t, -1, False, buf)
+        if rank > 0:
+            pending.append(dist.isend(buf, dst=rank - 1, group=group))
+    for w in pending:
+        w.wait()
