@@ -115,6 +115,13 @@ int vr_henyey_greenstein(uint32_t n, float g, float *out);
  * int*), zero-extended -- exactly the value the reference hands to MATLAB. */
 uint64_t vr_timestamp(void);
 
+/* Fused stereo: VolumeRender.render with CameraXOffset != 0
+ * (VolumeRender.m:278-307) renders the pair as two 'render' calls with camera offsets +base and
+ * -base.  This renders both eyes of the same frame in one launch: args->props[0] is ignored, the
+ * left image (offset -base) goes to out_left, the right (+base) to out_right, each [H, W, 3] as
+ * vr_render writes it, bit-identical to the two separate renders. */
+int vr_render_stereo(vr_context *h, const vr_render_args *args, float base, float *out_left, float *out_right);
+
 /* --- device-side extensions (multi-GPU, benchmarking; no MATLAB counterpart) ------------------ */
 
 /* 'render' without the host round trip: writes the (partitioned, if part != NULL) image to the

@@ -33,7 +33,7 @@ class Tee:
             h = self.hmap[int(args[0])]
             vols = [_ovol(v) for v in args[2:]]
             self.S.sync_volumes(h, int(args[1]), *vols)
-        elif cmd == "render":
+        elif cmd in ("render", "render_stereo"):
             h = self.hmap[int(args[0])]
             lights, illum = args[1], args[2]
             if isinstance(lights, (bool, np.bool_)) or isinstance(illum, (bool, np.bool_)):
@@ -42,13 +42,24 @@ class Tee:
                 seq = lights if isinstance(lights, (list, tuple)) else [lights]
                 L = np.array([list(l.Position) + list(l.Color) for l in seq], dtype=np.float32).reshape(-1, 6)
                 I = _ovol(illum)
-            rest = args[3:10]
-            # the f32 oracle mutates the session exactly like the product (light upload);
-            # the f64 envelope run repeats the same marshalling on the same state.
-            ref32, _ = self.S.render(h, L, I, *rest, threads=self.threads)
-            ref64, _ = self.S.render(h, L, I, *rest, double=True, threads=self.threads)
-            stats = assert_parity(out, ref32, ref64, what=f"render #{len(self.renders)}")
-            self.renders.append((out, ref32, stats))
+            rest = list(args[3:10])
+            if cmd == "render":
+                views = [(out, rest)]
+            else:  # the fused pair is the reference's two renders: right (+base), then left (-base)
+                base = np.float32(args[10])
+                left, right = out
+                views = []
+                for img, off in ((right, base), (left, -base)):
+                    props = np.array(rest[4], dtype=np.float32).reshape(-1).copy()  # [xoff f dist]
+                    props[0] = off
+                    views.append((img, rest[:4] + [props] + rest[5:]))
+            for img, r in views:
+                # the f32 oracle mutates the session exactly like the product (light upload);
+                # the f64 envelope run repeats the same marshalling on the same state.
+                ref32, _ = self.S.render(h, L, I, *r, threads=self.threads)
+                ref64, _ = self.S.render(h, L, I, *r, double=True, threads=self.threads)
+                stats = assert_parity(img, ref32, ref64, what=f"render #{len(self.renders)}")
+                self.renders.append((img, ref32, stats))
         return out
 
 

@@ -489,3 +489,19 @@ def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case
     assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
     assert not st[4].any()  # every ray finished
     r.delete()
+
+
+@pytest.mark.parametrize("lit", [True, False])
+def test_fused_stereo_equals_two_renders(monkeypatch, counter_clock, lit):
+    """Fused stereo: vr_render_stereo renders both eyes in one launch; the
+    images are those of the reference's two 'render' calls (VolumeRender.m:278-287), bit for bit."""
+    v = vr.Volume(O.shell_volume(44))
+    r = ex1_renderer(v, res=(90, 70), lights=lit)
+    r.CameraXOffset = 0.5
+    monkeypatch.setenv("VR_NO_FUSED_STEREO", "1")
+    two = r.render()
+    monkeypatch.delenv("VR_NO_FUSED_STEREO")
+    fused = r.render()
+    assert two.max() > 0 and two.shape == fused.shape
+    assert np.array_equal(np.asarray(two, np.float32).view(np.uint32), np.asarray(fused, np.float32).view(np.uint32))
+    r.delete()

@@ -75,6 +75,22 @@ def main():
     out = {"volume": n, "image": [W, H], "always_reupload": os.environ.get("VR_ALWAYS_REUPLOAD", "0"),
            "sync_s": round(t_sync, 3), "sync_GBps": round(host.nbytes / t_sync / 1e9, 2),
            "p_render_ms": round(med(p_render), 2)}
+    # stereo pair (example3.m CameraXOffset 0.06, f = 3 here): the reference's two renders vs the
+    # fused launch (vr_render_stereo); each at the widened resolution [H, W + delta]
+    base = 0.03
+    fov = 2 * np.arctan(1 / 3.0)
+    delta = int(np.floor(base * W / (2 * 3.0 * np.tan(fov / 2)) + 0.5))
+    scall = list(call)
+    scall[6] = np.uint64([H, W + delta])
+
+    def two_renders():
+        for off in (base, -base):
+            c = list(scall)
+            c[8] = np.float32([off, 3.0, 6.0])
+            vr.volumeRender(*c)
+
+    out["stereo_two_renders_ms"] = round(med(two_renders), 2)
+    out["stereo_fused_ms"] = round(med(lambda: vr.volumeRender("render_stereo", *scall[1:], np.float32(base))), 2)
     if not args.no_lookup:
         grads = em.grad() if n <= 256 else _device_grad(host, mex, vr)
         t0 = time.perf_counter()

@@ -62,6 +62,7 @@ SIGNATURES = [
     ("vr_sync_volumes", c_int, [c_void_p, c_uint64, POINTER(VrVolume), POINTER(VrVolume), POINTER(VrVolume),
                                 POINTER(VrVolume), POINTER(VrVolume), POINTER(VrVolume)]),
     ("vr_render", c_int, [c_void_p, POINTER(VrRenderArgs), c_void_p]),
+    ("vr_render_stereo", c_int, [c_void_p, POINTER(VrRenderArgs), c_float, c_void_p, c_void_p]),
     ("vr_henyey_greenstein", c_int, [c_uint32, c_float, c_void_p]),
     ("vr_timestamp", c_uint64, []),
     ("vr_render_device", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrPartition), c_void_p, c_void_p,

@@ -657,8 +657,11 @@ int depth_lanes(const vr::RenderParams &P) {
 }
 
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
+// d_out2 / eye2 (optional): fused stereo -- the same frame seen from a second eye position, into a
+// second image, in the same launch (vr_render_stereo).
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
-              unsigned long long *d_steps, hipStream_t stream, Frame &F) {
+              unsigned long long *d_steps, hipStream_t stream, Frame &F, float *d_out2 = nullptr,
+              const float *eye2 = nullptr) {
   if (a->num_lights > 0 && !a->lights) return fail(VR_ERR_ARGUMENT, "lights is NULL");
   uint64_t required = required_memory(h);
   if (a->num_lights >= 0 && a->illumination) {
@@ -700,8 +703,14 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
   if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
+  if (d_out2) {
+    P.views = 2;
+    P.out2 = d_out2;
+    for (int i = 0; i < 3; ++i) P.eye2[i] = eye2[i];
+  }
   if (F.degenerate) {
     if (out_bytes) VR_HIP(hipMemsetAsync(d_out, 0, out_bytes, stream));
+    if (out_bytes && d_out2) VR_HIP(hipMemsetAsync(d_out2, 0, out_bytes, stream));
     return VR_OK;
   }
   // LDS-staged march (vr_march.hip) whenever the emission texture is a real grid and, for the
@@ -752,7 +761,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     // the tail is a small part of the frame and the row-major order keeps neighbouring tiles (which
     // share voxels in L2) running together (metric frame: 43.6 ms row-major, 45.0 ms sorted).
     const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) / device_wave_slots();
-    const bool sched = env_flag("VR_SCHED") || (!env_flag_off("VR_SCHED") && rounds < VR_SCHED_ROUNDS);
+    const bool sched = P.views < 2 && (env_flag("VR_SCHED") || (!env_flag_off("VR_SCHED") && rounds < VR_SCHED_ROUNDS));
     if (!P.steps && sched && K > 1) {
       static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
                                         vr::fast::march_blocks_k4, vr::fast::march_blocks_k8};
@@ -787,6 +796,11 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
         if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
       }
     }
+    if (P.views > 1) {
+      static const blocks_fn vfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
+                                        vr::fast::march_blocks_k4, vr::fast::march_blocks_k8};
+      P.view_blocks = vfns[ki](P);
+    }
     VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
     if (P.wg_cost) {
       if (const char *dump = std::getenv("VR_SCHED_DUMP")) {  // diagnostics: append block durations
@@ -803,6 +817,11 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     }
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
+    if (P.views > 1) {  // the general kernel renders one view per launch
+      for (int i = 0; i < 3; ++i) P.eye[i] = P.eye2[i];
+      P.out = P.out2;
+      VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
+    }
   }
   return VR_OK;
 }
@@ -1026,6 +1045,42 @@ int vr_render(vr_context *h, const vr_render_args *a, float *out) {
   int rc = do_render(h, a, nullptr, h->d_out, nullptr, nullptr, F);
   if (rc) return rc;
   if (bytes) VR_HIP(hipMemcpy(out, h->d_out, bytes, hipMemcpyDeviceToHost));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_render_stereo(vr_context *h, const vr_render_args *a, float base, float *out_left, float *out_right) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  const size_t bytes = (size_t)a->resolution[0] * (size_t)a->resolution[1] * 3 * sizeof(float);
+  if (bytes && (!out_left || !out_right)) return fail(VR_ERR_ARGUMENT, "output is NULL");
+  if (2 * bytes > h->d_out_bytes) {
+    if (h->d_out) VR_HIP(hipFree(h->d_out));
+    h->d_out = nullptr;
+    h->d_out_bytes = 0;
+    VR_HIP(hipMalloc(&h->d_out, 2 * bytes));
+    h->d_out_bytes = 2 * bytes;
+  }
+  // left eye: camera x offset -base (the frame's own eye); right eye: +base, formed as build_frame
+  // forms it (fma(-dist, Z, xoff * X), render.cpp:211-221 column order)
+  vr_render_args al = *a;
+  al.props[0] = -base;
+  const float *r = a->rotation_flipped;
+  const float X[3] = {r[2], r[1], r[0]}, Z[3] = {r[8], r[7], r[6]};
+  const float dist = a->props[2];
+  float eye2[3];
+  for (int i = 0; i < 3; ++i) eye2[i] = fmaf(-dist, Z[i], base * X[i]);
+  Frame F;
+  float *d_left = h->d_out, *d_right = h->d_out + bytes / sizeof(float);
+  int rc = do_render(h, &al, nullptr, d_left, nullptr, nullptr, F, d_right, eye2);
+  if (rc) return rc;
+  if (bytes) {
+    VR_HIP(hipMemcpy(out_left, d_left, bytes, hipMemcpyDeviceToHost));
+    VR_HIP(hipMemcpy(out_right, d_right, bytes, hipMemcpyDeviceToHost));
+  }
   return VR_OK;
   VR_GUARD_END
 }

@@ -41,6 +41,7 @@ struct RenderParams {
   float bmin[3];                  // boxmin                              volumeRender.cpp:131
   float bscale[3];                // 1 / (boxmax - boxmin)               kernel.cu:396
   float eye[3];                   // xoff*X - dist*Z                     kernel.cu:407-410
+  float eye2[3];                  // fused stereo: the second view's eye (views == 2)
   float nx_[3];                   // normalize(X)                        kernel.cu:413
   float ydir[3], zdir[3];         // Y, Z columns
   float focal;                    // f
@@ -63,6 +64,9 @@ struct RenderParams {
   int32_t block_cols, part, num_parts, part_cols;
   int32_t plane_cols;             // column stride of the output planes (part 0's column count)
   float *out;                     // [3][plane_cols][H]: column-major planar image of the part
+  float *out2;                    // fused stereo: the second view's image
+  int32_t views;                  // 1, or 2 = both stereo eyes in one launch (vr_render_stereo)
+  uint32_t view_blocks;           // workgroups per view (the launch has views x view_blocks)
   // launch schedule: workgroup b marches tile block wg_order[b] (null: b); each
   // block's duration in s_memrealtime ticks is stored to wg_cost[block] (null: not recorded)
   const uint32_t *wg_order;

@@ -419,9 +419,13 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
   const uint64_t clk0 = SCHED ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint32_t wg = SCHED ? P.wg_order[blockIdx.x] : blockIdx.x;  // cost-ordered schedule
+  const uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : blockIdx.x;  // cost-ordered schedule
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
   if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
+  // fused stereo: the second view's workgroups follow the first's (same rays, other eye)
+  const int view = (P.views > 1 && wgo >= P.view_blocks) ? 1 : 0;
+  const uint32_t wg = view ? wgo - P.view_blocks : wgo;
+  float *const out = view ? P.out2 : P.out;
   const int tile = (int)wg * VR_WG_WAVES + wave;
   const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
   const int blk = tile >> 2, quad = tile & 3;
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
     f3 d;
     float tnear;
-    R.alive = ray_setup(P, x, y, R.o, d, tnear, R.tfar);
+    R.alive = ray_setup(P, x, y, R.o, d, tnear, R.tfar, view);
     R.pos = mk(fmaf(d.x, tnear, R.o.x), fmaf(d.y, tnear, R.o.y), fmaf(d.z, tnear, R.o.z));
     R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
     R.t = tnear;
@@ -458,15 +462,15 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   if (active && (lane & (K - 1)) == 0) {
     const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
     const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
-    P.out[kk] = R.sr;
-    P.out[kk + plane] = R.sg;
-    P.out[kk + 2 * plane] = R.sb;
+    out[kk] = R.sr;
+    out[kk + plane] = R.sg;
+    out[kk + 2 * plane] = R.sb;
   }
   if (SCHED) {  // this block's duration, for the next launch's schedule
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
-      P.wg_cost[wg] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+      P.wg_cost[wgo] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
     }
   }
   if (COUNT) {
@@ -621,7 +625,9 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
   if (VR_MARCH_K != 1 && P.steps) return hipErrorInvalidValue;
   const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
-  const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES));
+  const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
+  if (P.views > 1 && (P.view_blocks != per_view || !P.out2)) return hipErrorInvalidValue;
+  const dim3 grid(per_view * (P.views > 1 ? 2u : 1u));
   if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || VR_MARCH_K == 1))
     return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {

@@ -225,10 +225,10 @@ __device__ __forceinline__ bool tile_of_block(const RenderParams &P, int &tx, in
 // Primary ray of pixel (x, y) and its box intersection (volumeRender_kernel.cu:388-425), op for
 // op as the oracle.  Returns hit; tnear is already clamped to 0.
 __device__ __forceinline__ bool ray_setup(const RenderParams &P, int x, int y, f3 &o, f3 &d, float &tnear,
-                                          float &tfar) {
+                                          float &tfar, int view = 0) {
   const float u = fmaf((float)x / P.fw, 2.f, -1.f);
   const float v = fmaf(((float)y / P.fh) * 2.f, P.ratio, -P.ratio);
-  o = mk(P.eye[0], P.eye[1], P.eye[2]);
+  o = view ? mk(P.eye2[0], P.eye2[1], P.eye2[2]) : mk(P.eye[0], P.eye[1], P.eye[2]);
   f3 du;
   du.x = fmaf(P.focal, P.zdir[0], fmaf(v, P.ydir[0], u * P.nx_[0]));
   du.y = fmaf(P.focal, P.zdir[1], fmaf(v, P.ydir[1], u * P.nx_[1]));

@@ -278,6 +278,17 @@ def volumeRender(cmd, *args):
         if nrhs > 9:
             warnings.warn("SyncVolumes: Unexpected arguments ignored.")
         return None
+    if cmd == "render_stereo":  # fused stereo pair (vr_render_stereo): args as 'render' + base
+        ra, keep = render_args(*args[1:10])
+        res = np.asarray(args[5]).reshape(-1)
+        H, W = int(res[0]), int(res[1])
+        left = np.zeros((H, W, 3), dtype=np.float32, order="F")
+        right = np.zeros((H, W, 3), dtype=np.float32, order="F")
+        check(L.vr_render_stereo(h, ctypes.byref(ra), float(args[10]),
+                                 left.ctypes.data_as(ctypes.c_void_p) if left.size else None,
+                                 right.ctypes.data_as(ctypes.c_void_p) if right.size else None))
+        del keep
+        return left, right
     if cmd == "render":
         if nrhs < 11:
             raise _lib.VrError(1, "insufficient parameter!")

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import enum
 import math
+import os
 import warnings
 
 import numpy as np
@@ -158,8 +159,11 @@ class VolumeRender:
         delta = base * self.ImageResolution[1] / (2 * self.FocalLength * math.tan(fov / 2))
         delta = int(math.floor(abs(delta) + 0.5)) * (1 if delta >= 0 else -1)  # MATLAB round
         resolution = res + np.array([0, delta])
-        right = self._p_render(base, resolution)
-        left = self._p_render(-base, resolution)
+        if os.environ.get("VR_NO_FUSED_STEREO") == "1":  # the reference's two renders
+            right = self._p_render(base, resolution)
+            left = self._p_render(-base, resolution)
+        else:  # both eyes in one launch (vr_render_stereo), the same images
+            left, right = self._p_render(np.float32(base), resolution, stereo=True)
         left = _imcrop(left, delta + 1, left.shape[1])
         right = _imcrop(right, 0, right.shape[1] - delta)
         if self.StereoOutput == StereoRenderMode.RedCyan:
@@ -170,8 +174,8 @@ class VolumeRender:
             return img
         return np.asfortranarray(np.concatenate([left, right], axis=1))
 
-    def _p_render(self, camera_x_offset, resolution) -> np.ndarray:
-        """VolumeRender.m:497-583."""
+    def _p_render(self, camera_x_offset, resolution, stereo=False):
+        """VolumeRender.m:497-583 (stereo=True: both eyes at +-camera_x_offset, one launch)."""
         validate = [_is_logical(self.VolumeReflection), _is_logical(self.VolumeAbsorption),
                     _is_logical(self.VolumeEmission)]
         if _is_logical(self.VolumeIllumination):
@@ -192,6 +196,9 @@ class VolumeRender:
                 factors.astype(np.float32), self.ElementSizeUm.astype(np.float32),
                 np.asarray(resolution).astype(np.uint64), matrix.astype(np.float32),
                 props.astype(np.float32), np.float32(self.OpacityThreshold), self.Color.astype(np.float32)]
+        if stereo:
+            args[0] = "render_stereo"
+            return volumeRender(*(args + [np.float32(camera_x_offset)]))
         if with_grads:
             args += grads
         return volumeRender(*args)
