@@ -387,14 +387,16 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
   return fabsf(v.x) <= 3.4e38f && fabsf(v.y) <= 3.4e38f && fabsf(v.z) <= 3.4e38f;
 }
 
-// Occupancy of the march: 6 KiB wave slots fit 6 workgroups (24 waves) per CU, which 80 VGPRs
-// allow (6 waves per SIMD; ~2 VGPRs spill).  Measured on MI355X: the metric frame 43.8 -> 42.6 ms
-// (K = 2).  A scheduled launch (few rounds, heavy waves first) keeps the uncapped allocation: its
+// Occupancy of the march: 6.5 KiB wave slots (1664 floats, the largest for which six 4-wave
+// workgroups fit the 160 KiB LDS at its allocation granularity) fit 6 workgroups (24 waves) per
+// CU, which 80 VGPRs allow (6 waves per SIMD; ~2 VGPRs spill).  Measured on MI355X: the metric
+// frame 43.8 ms (10 KiB, 16 waves) -> 42.6 (6 KiB) -> 41.2 (6.5 KiB; 1704 floats: 5 workgroups,
+// 41.9) at K = 2.  A scheduled launch (few rounds, heavy waves first) keeps the uncapped allocation: its
 // longest waves share a SIMD with fewer others (one rank's share at P = 8: 7.2 ms vs 7.7 capped).
 #ifndef VR_MARCH_MIN_EU
 #define VR_MARCH_MIN_EU 6
 #endif
-constexpr int march_min_eu(int cap, bool sched) { return (cap <= 1536 && !sched) ? VR_MARCH_MIN_EU : 1; }
+constexpr int march_min_eu(int cap, bool sched) { return (cap <= 1664 && !sched) ? VR_MARCH_MIN_EU : 1; }
 #ifndef VR_WG_WAVES
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif

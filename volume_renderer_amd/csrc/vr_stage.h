@@ -16,7 +16,7 @@ namespace vr {
 // Wave slot sizes (floats).  The march kernel is built for both and the host picks per frame
 // from the camera's texels per pixel (vr_capi.hip): the 8x8-ray footprint grows with it.
 #ifndef VR_LDS_CAP
-#define VR_LDS_CAP 1536        // 6 KiB: 24 KiB per workgroup -> 6 workgroups (24 waves) per CU
+#define VR_LDS_CAP 1664        // 6.5 KiB: 26 KiB per workgroup -> 6 workgroups (24 waves) per CU
 #endif
 #ifndef VR_LDS_CAP_WIDE
 #define VR_LDS_CAP_WIDE 3072   // 12 KiB: 3 workgroups per CU, for footprints above ~1.5 texels/pixel
