@@ -8,7 +8,12 @@ threshold 0.9, camera rotate(125,25,0), f=3, dist=6, reflection = the class defa
 
 A "step" = one frame: the ray-march kernel over this rank's image columns (+ at N>1 the RCCL
 gather of the column partitions to rank 0 and the on-device assembly of the full image).
-Volumes are resident in HBM before the timed region (sync_volumes is not timed).
+Volumes are resident in HBM before the timed region (sync_volumes is not timed).  The K timed
+frames are independent (a movie, examples/example3.m) and are issued round-robin on --streams HIP
+streams (default 2), each with its own output buffers, so that one frame's tail -- its longest
+waves -- overlaps the next frame's start; `value` / `ms_per_step` are that throughput.  A serial
+pass of K frames (one after the other) runs first: its HIP-event kernel times give
+roofline.kernel_ms / achieved, and its wall time is `serial_ms_per_step`.
 Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
 """
 from __future__ import annotations
@@ -46,7 +51,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1024, help="volume edge (metric config: 1024)")
+    ap.add_argument("--volume", type=int, default=1024, help="V_shell edge (metric config: 1024); not --n, which torch.distributed.run would take for its own --nnodes")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--block-cols", type=int, default=16, help="column block of the image partition")
@@ -61,6 +66,11 @@ def main():
     ap.add_argument("--sim-parts", type=int, default=0,
                     help="diagnostic (1 GPU): also time each rank's share of a P-way column partition, "
                          "the kernel time a rank would see at --gpus P")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the timed frames are issued on round-robin: frames are independent (a "
+                         "movie, example3.m), so one frame's tail -- its longest waves -- overlaps the next "
+                         "frame's start.  1: strictly one frame after the other.  The kernel time of the "
+                         "roofline always comes from a serial pass.")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round1", "traffic.json"),
                     help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
@@ -81,7 +91,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    n, W, H = args.n, args.width, args.height
+    n, W, H = args.volume, args.width, args.height
 
     # ---- inputs, resident in HBM before timing ------------------------------------------------
     vol_t = torch.empty(n * n * n, dtype=torch.float32, device=dev)
@@ -162,6 +172,40 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
 
+    serial_elapsed = elapsed
+    if args.streams > 1:
+        ns = args.streams
+        streams = [torch.cuda.Stream(dev) for _ in range(ns)]
+        outs = [torch.zeros_like(out_local) for _ in range(ns)]
+        fulls = [torch.zeros(3 * W * H, dtype=torch.float32, device=dev) for _ in range(ns)] if rank == 0 else None
+        gaths = ([torch.zeros_like(gathered) for _ in range(ns)] if (world > 1 and rank == 0) else None)
+
+        def oframe(i):
+            j = i % ns
+            mex.render_device(h, ra, outs[j].data_ptr(), part, 0, streams[j].cuda_stream)
+            if world > 1:  # gather + assembly on the default stream, after this frame's kernel only
+                stream.wait_stream(streams[j])
+                dist.gather(outs[j], list(gaths[j].chunk(world)) if rank == 0 else None, dst=0)
+                if rank == 0:
+                    mex.assemble_partitions(gaths[j].data_ptr(), W, H, args.block_cols, world, max_cols,
+                                            fulls[j].data_ptr(), sptr)
+                streams[j].wait_stream(stream)  # the buffers of frame i are reused by frame i + ns
+
+        for i in range(max(args.warmup, 2 * ns)):  # every stream's schedule measured (vr_capi.hip)
+            oframe(i)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            oframe(i)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t1
+
     sim = None
     if args.sim_parts > 1 and world == 1:
         P_ = args.sim_parts
@@ -178,14 +222,24 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize(dev)
             sim.append(round(e0.elapsed_time(e1) / 3, 3))
+            if args.streams > 1:  # the same share, launches alternating over streams
+                ss = [torch.cuda.Stream(dev) for _ in range(args.streams)]
+                for k in range(2 * len(ss)):  # each stream's first launch measures its schedule
+                    mex.render_device(h, ra, sim_out.data_ptr(), pp, 0, ss[k % len(ss)].cuda_stream)
+                torch.cuda.synchronize(dev)
+                t2 = time.perf_counter()
+                for k in range(6):
+                    mex.render_device(h, ra, sim_out.data_ptr(), pp, 0, ss[k % len(ss)].cuda_stream)
+                torch.cuda.synchronize(dev)
+                sim[-1] = (sim[-1], round((time.perf_counter() - t2) / 6 * 1e3, 3))
         del sim_out
 
     samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=dev)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed, serial_elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(samples_all, op=dist.ReduceOp.SUM)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed, serial_elapsed = float(el[0].item()), float(el[1].item())
     total_samples = int(samples_all[0].item())
     total_lit = int(samples_all[1].item())
 
@@ -234,9 +288,16 @@ def main():
                          "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F},
             "cpu_baseline": None,
         }
+        result["streams"] = args.streams
+        result["serial_ms_per_step"] = round(serial_elapsed / args.steps * 1e3, 3)
         if sim is not None:
-            result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
-                                             "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
+            if args.streams > 1:
+                result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part_serial_overlapped": sim,
+                                                 "max_serial": max(x[0] for x in sim),
+                                                 "max_overlapped": max(x[1] for x in sim)}
+            else:
+                result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
+                                                 "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
 
     # ---- CPU baseline: the oracle (C, OpenMP) on every k-th column of the same frame -----------
     if rank == 0 and world == 1 and host_vol is not None:
