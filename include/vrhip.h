@@ -122,6 +122,33 @@ uint64_t vr_timestamp(void);
  * vr_render writes it, bit-identical to the two separate renders. */
 int vr_render_stereo(vr_context *h, const vr_render_args *args, float base, float *out_left, float *out_right);
 
+/* Multi-channel frame (replaces the per-channel loops of examples/example3.m:
+ * 61-233 -- sync a channel's volumes, render, next channel -- and the sum at example3.m:239).  A
+ * channel is one VolumeRender object: its handle (distinct per channel), the arguments of its
+ * 'sync_volumes' (volumeRender.cpp:600-633; dx/dy/dz NULL = on-the-fly gradient) and of its
+ * 'render'.  Channel i equals vr_sync_volumes + vr_render on it, in channel order (stereo != 0:
+ * vr_render_stereo with `base`, left then right); every channel must have the same resolution.
+ * The channels' frames are marched together (one launch per gradient-mode / absorption / shading
+ * group).  vr_render_channels writes channel i's view e (e = 0 left / only, 1 right; eyes = 1 or
+ * 2) to out[(i * eyes + e) * H*W*3 ...], each laid out as vr_render's image; the caller adds them
+ * (example3.m:239 adds in double). */
+typedef struct vr_channel {
+  vr_context *handle;
+  uint64_t time_last_mem_sync;
+  const vr_volume *emission, *reflection, *absorption;
+  const vr_volume *dx, *dy, *dz;
+  const vr_render_args *args;
+} vr_channel;
+int vr_render_channels(const vr_channel *channels, int32_t n, int32_t stereo, float base, float *out);
+/* Device variant: channel i's view e (e = 0 left / only, 1 right) into
+ * d_out + (i * eyes + e) * H*W*3, on `stream` (asynchronous; the syncs are not). */
+int vr_render_channels_device(const vr_channel *channels, int32_t n, int32_t stereo, float base, float *d_out,
+                              void *stream);
+/* fp32 channel sum on the device: d_out[e][k] = d_in[0][e][k] + d_in[1][e][k] + ... (channel order,
+ * fp32 additions) for n channels x views images of image_floats floats each. */
+int vr_sum_channels_device(const float *d_in, int32_t n, int32_t views, uint64_t image_floats, float *d_out,
+                           void *stream);
+
 /* --- device-side extensions (multi-GPU, benchmarking; no MATLAB counterpart) ------------------ */
 
 /* 'render' without the host round trip: writes the (partitioned, if part != NULL) image to the

@@ -505,3 +505,80 @@ def test_fused_stereo_equals_two_renders(monkeypatch, counter_clock, lit):
     assert two.max() > 0 and two.shape == fused.shape
     assert np.array_equal(np.asarray(two, np.float32).view(np.uint32), np.asarray(fused, np.float32).view(np.uint32))
     r.delete()
+
+
+def _channel_pair(lit):
+    """Two channels of an examples/example3.m-style frame: the main channel (V_shell) and a
+    structure channel (a second field) with their own colour and factors, one object each."""
+    n = 40
+    g = np.linspace(-1.0, 1.0, n, dtype=np.float32)
+    X, Y, Z = np.meshgrid(g, g, g, indexing="ij")
+    blob = np.asfortranarray(np.exp(-4.0 * ((X - 0.2) ** 2 + (Y + 0.1) ** 2 + Z ** 2)).astype(np.float32))
+    main = ex1_renderer(vr.Volume(O.shell_volume(n)), res=(90, 70), lights=lit)
+    struct = ex1_renderer(vr.Volume(blob), res=(90, 70), lights=lit)
+    struct.Color = [0, 1, 0]
+    struct.FactorEmission = 0.5
+    struct.FactorAbsorption = 1.0
+    return main, struct
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lit", [True, False])
+@pytest.mark.parametrize("stereo", [False, True])
+def test_fused_channels_equal_separate_renders(monkeypatch, counter_clock, lit, stereo):
+    """Multi-channel frame: VolumeRender.renderChannels marches the channels
+    (x both stereo eyes) in one launch; each channel's image is bit for bit what its own render()
+    gives (the reference renders the channels one after the other, examples/example3.m)."""
+    def pair():  # fresh objects and volumes: every channel's sync uploads (see below)
+        rs = _channel_pair(lit)
+        for r in rs:
+            r.CameraXOffset = 0.5 if stereo else 0
+        return rs
+
+    # (objects stay referenced: 'delete' resets every handle's device state: ~MManager -> cudaDeviceReset)
+    main, struct = pair()
+    sep = [main.render(), struct.render()]
+    fp, up = pair(), None
+    fused = vr.VolumeRender.renderChannels(list(fp))
+    monkeypatch.setenv("VR_NO_FUSED_CHANNELS", "1")
+    up = pair()
+    unfused = vr.VolumeRender.renderChannels(list(up))
+    monkeypatch.delenv("VR_NO_FUSED_CHANNELS")
+    bits = lambda x: np.asarray(x, np.float32).view(np.uint32)
+    for a, b, c in zip(sep, fused, unfused):
+        assert a.max() > 0 and a.shape == b.shape == c.shape
+        assert np.array_equal(bits(a), bits(b))
+        assert np.array_equal(bits(a), bits(c))
+    # The reference's textures are module globals and its upload dedup is per object
+    # (mmanager.hxx:178-201): an object whose volumes did not change since its last sync renders
+    # with the textures another object bound last.  The channels reproduce that, as the sequence
+    # sync + render per channel would.
+    again = vr.VolumeRender.renderChannels([main, struct])
+    seq = [main.render(), struct.render()]
+    for a, b in zip(again, seq):
+        assert a.max() > 0
+        assert np.array_equal(bits(a), bits(b))
+    for r in (main, struct) + fp + up:
+        r.delete()
+
+
+@pytest.mark.gpu
+def test_channels_mixed_gradient_modes(monkeypatch, counter_clock):
+    """A lookup-gradient channel (not marched in the fused launch) beside an on-the-fly one: each
+    is rendered against its own synced textures, identical to its own render()."""
+    def pair():
+        main, struct = _channel_pair(True)
+        gy, gx, gz = np.gradient(np.asarray(struct.VolumeEmission.Data, np.float64))
+        for name, gvol in (("VolumeGradientX", gx), ("VolumeGradientY", gy), ("VolumeGradientZ", gz)):
+            setattr(struct, name, vr.Volume(np.asfortranarray(gvol.astype(np.float32))))
+        return main, struct
+
+    main, struct = pair()
+    sep = [main.render(), struct.render()]
+    fp = pair()
+    fused = vr.VolumeRender.renderChannels(list(fp))
+    for r in (main, struct) + fp:
+        r.delete()
+    for a, b in zip(sep, fused):
+        assert a.max() > 0
+        assert np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))

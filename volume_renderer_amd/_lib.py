@@ -44,6 +44,13 @@ class VrPartition(ctypes.Structure):
                 ("reserved", c_int32)]
 
 
+class VrChannel(ctypes.Structure):
+    _fields_ = [("handle", c_void_p), ("time_last_mem_sync", c_uint64),
+                ("emission", POINTER(VrVolume)), ("reflection", POINTER(VrVolume)),
+                ("absorption", POINTER(VrVolume)), ("dx", POINTER(VrVolume)), ("dy", POINTER(VrVolume)),
+                ("dz", POINTER(VrVolume)), ("args", POINTER(VrRenderArgs))]
+
+
 class VrError(RuntimeError):
     """A non-zero status from libvrhip; ``code`` is the vr_status value."""
 
@@ -63,6 +70,9 @@ SIGNATURES = [
                                 POINTER(VrVolume), POINTER(VrVolume), POINTER(VrVolume)]),
     ("vr_render", c_int, [c_void_p, POINTER(VrRenderArgs), c_void_p]),
     ("vr_render_stereo", c_int, [c_void_p, POINTER(VrRenderArgs), c_float, c_void_p, c_void_p]),
+    ("vr_render_channels", c_int, [POINTER(VrChannel), c_int32, c_int32, c_float, c_void_p]),
+    ("vr_render_channels_device", c_int, [POINTER(VrChannel), c_int32, c_int32, c_float, c_void_p, c_void_p]),
+    ("vr_sum_channels_device", c_int, [c_void_p, c_int32, c_int32, c_uint64, c_void_p, c_void_p]),
     ("vr_henyey_greenstein", c_int, [c_uint32, c_float, c_void_p]),
     ("vr_timestamp", c_uint64, []),
     ("vr_render_device", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrPartition), c_void_p, c_void_p,

@@ -22,6 +22,7 @@
 #include <mutex>
 #include <map>
 #include <set>
+#include <array>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -39,6 +40,9 @@ hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool bi
   hipError_t launch_march_k4(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
   hipError_t launch_march_k8(const RenderParams &, int, bool, bool, bool, hipStream_t);                  \
   hipError_t launch_march_slab_k1(const RenderParams &, int, hipStream_t);                                \
+  hipError_t launch_march_views_k1(const RenderViews &, uint32_t, int, bool, hipStream_t);                 \
+  hipError_t launch_march_views_k2(const RenderViews &, uint32_t, int, bool, hipStream_t);                 \
+  hipError_t launch_march_views_k4(const RenderViews &, uint32_t, int, bool, hipStream_t);                 \
   hipError_t launch_march_slab_k2(const RenderParams &, int, hipStream_t);                                \
   hipError_t launch_march_slab_k4(const RenderParams &, int, hipStream_t);                                \
   uint32_t march_blocks_k1(const RenderParams &);                                                        \
@@ -54,6 +58,7 @@ hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
+hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
 hipError_t launch_synth_shell(float *out, uint64_t n, uint64_t z_first, uint64_t nz, hipStream_t s);
@@ -163,6 +168,12 @@ struct vr_context {
     bool measured = false;
   };
   std::map<std::string, Schedule> sched;
+  // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
+  void *d_views = nullptr;
+  size_t d_views_bytes = 0;
+  std::vector<unsigned char> h_views;  // host image of d_views (alive until the copy has run)
+  float *d_chan = nullptr;             // per-view images of the host entry
+  size_t d_chan_bytes = 0;
 };
 
 namespace {
@@ -619,6 +630,15 @@ void set_chunk_halo(Frame &F, int K) {
   for (int i = 0; i < 3; ++i) F.P.tap_off[i] += (float)(chunk_samples(K) * F.drift1[i]);
 }
 
+void free_views(vr_context *h) {
+  if (h->d_views) (void)hipFree(h->d_views);
+  h->d_views = nullptr;
+  h->d_views_bytes = 0;
+  if (h->d_chan) (void)hipFree(h->d_chan);
+  h->d_chan = nullptr;
+  h->d_chan_bytes = 0;
+}
+
 void free_schedules(vr_context *h) {
   for (auto &kv : h->sched) {
     if (kv.second.d_cost) (void)hipFree(kv.second.d_cost);
@@ -659,9 +679,13 @@ int depth_lanes(const vr::RenderParams &P) {
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
 // d_out2 / eye2 (optional): fused stereo -- the same frame seen from a second eye position, into a
 // second image, in the same launch (vr_render_stereo).
+// fusable (optional, vr_render_channels): a frame the multi-view march can take (staged march,
+// gradient mode 0/1, 32-bit addressing) is only prepared -- F.P complete, *fusable = 1, nothing
+// launched; any other frame is rendered here as usual and *fusable = 0.
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
               unsigned long long *d_steps, hipStream_t stream, Frame &F, float *d_out2 = nullptr,
-              const float *eye2 = nullptr) {
+              const float *eye2 = nullptr, int *fusable = nullptr) {
+  if (fusable) *fusable = 0;
   if (a->num_lights > 0 && !a->lights) return fail(VR_ERR_ARGUMENT, "lights is NULL");
   uint64_t required = required_memory(h);
   if (a->num_lights >= 0 && a->illumination) {
@@ -744,6 +768,10 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       }
     }
     if (g_tex.gvec) P.gvec = g_tex.gvec->ptr;
+  }
+  if (fusable && march && F.mode <= 1 && !F.big && !P.steps) {
+    *fusable = 1;
+    return VR_OK;
   }
   if (march) {
     const int K = P.steps ? 1 : depth_lanes(P);  // the counter variant exists for K = 1
@@ -936,6 +964,7 @@ int vr_delete(vr_context *h) {
     c->d_out = nullptr;
     c->d_out_bytes = 0;
     free_schedules(c);
+    free_views(c);
   }
   g_contexts.erase(h);
   h->signature = 0;
@@ -986,10 +1015,9 @@ int vr_mem_info(vr_context *h, char *buf, size_t buflen) {
   VR_GUARD_END
 }
 
-int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume *emission,
+static int do_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume *emission,
                     const vr_volume *reflection, const vr_volume *absorption, const vr_volume *dx,
                     const vr_volume *dy, const vr_volume *dz) {
-  std::lock_guard<std::mutex> lk(g_mu);
   if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
   if (!emission || !reflection || !absorption) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
   const bool lookup = dx && dy && dz;
@@ -1022,6 +1050,179 @@ int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume 
   g_tex.grad_method = lookup ? G_LOOKUP : G_COMPUTE;  // setGradientMethod (render.cpp:121)
   mm_sync(h);
   VR_HIP(hipDeviceSynchronize());
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume *emission,
+                    const vr_volume *reflection, const vr_volume *absorption, const vr_volume *dx,
+                    const vr_volume *dy, const vr_volume *dz) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return do_sync_volumes(h, time_last_mem_sync, emission, reflection, absorption, dx, dy, dz);
+}
+
+// Multi-channel render (vr_render_channels): channel i is what vr_sync_volumes +
+// vr_render (or vr_render_stereo) on ch[i] in channel order would produce -- the syncs run in that
+// order, each channel's frame is prepared against the textures its own sync bound, and the frames
+// the staged march can take are marched together in one launch per (gradient mode, absorption
+// aliasing, slot size, shading) group, their views' parameters in device memory.  The buffers a
+// prepared frame reads stay referenced until the call returns; a later channel's sync never
+// overwrites them (each handle owns its buffers).
+static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, float base, float *d_out,
+                              hipStream_t stream) {
+  if (!ch || n < 1) return fail(VR_ERR_ARGUMENT, "no channels");
+  const int nv = stereo ? 2 : 1;
+  if (n * nv > VR_VIEWS_MAX) return fail(VR_ERR_ARGUMENT, "too many channels");
+  for (int i = 0; i < n; ++i) {
+    if (!valid(ch[i].handle)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+    if (!ch[i].args) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+    for (int j = 0; j < i; ++j)
+      if (ch[j].handle == ch[i].handle) return fail(VR_ERR_ARGUMENT, "channels need distinct handles");
+    if (ch[i].args->resolution[0] != ch[0].args->resolution[0] || ch[i].args->resolution[1] != ch[0].args->resolution[1])
+      return fail(VR_ERR_ARGUMENT, "channels differ in image resolution");
+    if (ch[i].handle->device != ch[0].handle->device) return fail(VR_ERR_ARGUMENT, "channels on different devices");
+  }
+  const size_t img = (size_t)ch[0].args->resolution[0] * (size_t)ch[0].args->resolution[1] * 3;
+  if (img && !d_out) return fail(VR_ERR_ARGUMENT, "output is NULL");
+  const bool fuse = !env_flag("VR_NO_FUSED_CHANNELS");
+  std::vector<BufPtr> keep;
+  std::vector<vr::RenderParams> views;
+  std::vector<std::array<double, 3>> drift;
+  std::vector<int> vmode, vab;
+  std::vector<vr::DevLight> lights;
+  std::vector<size_t> loff;
+  for (int i = 0; i < n; ++i) {
+    vr_context *h = ch[i].handle;
+    int rc = do_sync_volumes(h, ch[i].time_last_mem_sync, ch[i].emission, ch[i].reflection, ch[i].absorption,
+                             ch[i].dx, ch[i].dy, ch[i].dz);
+    if (rc) return rc;
+    vr_render_args a = *ch[i].args;
+    float eye2[3] = {0.f, 0.f, 0.f};
+    if (stereo) {  // as vr_render_stereo: left = the frame's eye at -base, right at +base
+      a.props[0] = -base;
+      const float *r = a.rotation_flipped;
+      const float X[3] = {r[2], r[1], r[0]}, Z[3] = {r[8], r[7], r[6]};
+      for (int k = 0; k < 3; ++k) eye2[k] = fmaf(-a.props[2], Z[k], base * X[k]);
+    }
+    float *dl = d_out + (size_t)i * nv * img, *dr = stereo ? dl + img : nullptr;
+    Frame F;
+    int fz = 0;
+    rc = do_render(h, &a, nullptr, dl, nullptr, stream, F, dr, stereo ? eye2 : nullptr, fuse ? &fz : nullptr);
+    if (rc) return rc;
+    if (!fz) continue;  // rendered by its own launch against the textures bound now
+    for (const BufPtr &b : g_tex.bind)
+      if (b) keep.push_back(b);
+    for (int v = 0; v < nv; ++v) {
+      vr::RenderParams P = F.P;
+      P.views = 1;
+      P.out2 = nullptr;
+      P.view_blocks = 0;
+      P.out = v ? dr : dl;
+      if (v)
+        for (int k = 0; k < 3; ++k) P.eye[k] = eye2[k];
+      views.push_back(P);
+      drift.push_back({F.drift1[0], F.drift1[1], F.drift1[2]});
+      vmode.push_back(F.mode);
+      vab.push_back(F.ab_alias ? 1 : 0);
+      loff.push_back(lights.size());
+    }
+    lights.insert(lights.end(), g_tex.lights.begin(), g_tex.lights.end());
+  }
+  if (views.empty()) return VR_OK;
+  // group the views by launch variant (contiguous in device memory), in channel order within a group
+  const size_t nvw = views.size();
+  std::vector<size_t> order(nvw);
+  for (size_t k = 0; k < nvw; ++k) order[k] = k;
+  auto key = [&](size_t k) {
+    return ((vmode[k] * 2 + vab[k]) * 2 + views[k].wide_slot) * 2 + views[k].fast_shade;
+  };
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return key(x) < key(y); });
+  vr_context *h0 = ch[0].handle;
+  // the views' lights in device memory (the global light buffer holds the last channel's only)
+  const size_t bytes = std::max<size_t>(lights.size(), 1) * sizeof(vr::DevLight);
+  if (bytes > h0->d_views_bytes) {
+    if (h0->d_views) VR_HIP(hipFree(h0->d_views));
+    h0->d_views = nullptr;
+    h0->d_views_bytes = 0;
+    VR_HIP(hipMalloc(&h0->d_views, bytes));
+    h0->d_views_bytes = bytes;
+  }
+  vr::DevLight *d_lights = static_cast<vr::DevLight *>(h0->d_views);
+  // the last sync waited for the device, so no earlier launch still reads d_views
+  h0->h_views.assign(bytes, 0);
+  if (!lights.empty()) std::memcpy(h0->h_views.data(), lights.data(), lights.size() * sizeof(vr::DevLight));
+  VR_HIP(hipMemcpyAsync(h0->d_views, h0->h_views.data(), bytes, hipMemcpyHostToDevice, stream));
+  typedef hipError_t (*views_fn)(const vr::RenderViews &, uint32_t, int, bool, hipStream_t);
+  static const views_fn vfns[2][3] = {
+      {vr::exact::launch_march_views_k1, vr::exact::launch_march_views_k2, vr::exact::launch_march_views_k4},
+      {vr::fast::launch_march_views_k1, vr::fast::launch_march_views_k2, vr::fast::launch_march_views_k4}};
+  size_t g0 = 0;
+  while (g0 < nvw) {
+    size_t g1 = g0;
+    while (g1 < nvw && key(order[g1]) == key(order[g0])) ++g1;
+    vr::RenderParams T = views[order[g0]];
+    T.height *= (int32_t)(g1 - g0);  // the group's waves decide the depth lanes
+    const int K = std::min(depth_lanes(T), 4);
+    vr::RenderViews V;
+    std::memset(&V, 0, sizeof V);
+    for (size_t k = g0; k < g1; ++k) {
+      vr::RenderParams &P = V.p[k - g0];
+      P = views[order[k]];
+      for (int d = 0; d < 3; ++d) P.tap_off[d] += (float)(chunk_samples(K) * drift[order[k]][d]);
+      P.lights = d_lights + loff[order[k]];
+    }
+    const size_t v0 = order[g0];
+    VR_HIP(vfns[views[v0].fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](V, (uint32_t)(g1 - g0), vmode[v0],
+                                                                              vab[v0] != 0, stream));
+    g0 = g1;
+  }
+  // a prepared frame's buffer that no handle or binding holds any more is freed on return: wait for
+  // the launches first (the handles' own buffers stay alive, the launches stay asynchronous)
+  bool orphan = false;
+  for (const BufPtr &b : keep) orphan = orphan || b.use_count() == 1;
+  if (orphan) VR_HIP(hipStreamSynchronize(stream));
+  return VR_OK;
+}
+
+int vr_render_channels_device(const vr_channel *ch, int32_t n, int32_t stereo, float base, float *d_out,
+                              void *stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!ch || n < 1 || !valid(ch[0].handle)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(ch[0].handle->device);
+  return do_render_channels(ch, n, stereo, base, d_out, (hipStream_t)stream);
+  VR_GUARD_END
+}
+
+int vr_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, float base, float *out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!ch || n < 1 || !valid(ch[0].handle)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!ch[0].args) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  VR_GUARD_BEGIN
+  vr_context *h = ch[0].handle;
+  DeviceGuard dg(h->device);
+  const size_t img = (size_t)ch[0].args->resolution[0] * (size_t)ch[0].args->resolution[1] * 3;
+  if (img && !out) return fail(VR_ERR_ARGUMENT, "output is NULL");
+  const size_t bytes = img * sizeof(float) * (size_t)n * (stereo ? 2 : 1);
+  if (bytes > h->d_chan_bytes) {
+    if (h->d_chan) VR_HIP(hipFree(h->d_chan));
+    h->d_chan = nullptr;
+    h->d_chan_bytes = 0;
+    VR_HIP(hipMalloc(&h->d_chan, bytes));
+    h->d_chan_bytes = bytes;
+  }
+  int rc = do_render_channels(ch, n, stereo, base, h->d_chan, nullptr);
+  if (rc) return rc;
+  if (bytes) VR_HIP(hipMemcpy(out, h->d_chan, bytes, hipMemcpyDeviceToHost));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_sum_channels_device(const float *d_in, int32_t n, int32_t views, uint64_t image_floats, float *d_out,
+                           void *stream) {
+  if (!d_in || !d_out || n < 1 || views < 1) return fail(VR_ERR_ARGUMENT, "invalid channel sum");
+  VR_GUARD_BEGIN
+  VR_HIP(vr::launch_sum_channels(d_in, (uint32_t)n, (uint32_t)views, image_floats, d_out, (hipStream_t)stream));
   return VR_OK;
   VR_GUARD_END
 }

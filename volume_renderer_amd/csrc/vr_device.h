@@ -83,6 +83,13 @@ struct RenderParams {
   const float *slab_in;
 };
 
+// The views of one multi-view launch (vr_render_channels), passed by value: 4 x 832 B of kernel
+// arguments.
+#define VR_VIEWS_MAX 4
+struct RenderViews {
+  RenderParams p[VR_VIEWS_MAX];
+};
+
 // Per-buffer statistics computed on the device at upload (used to prove the empty-sample skip
 // exact): any non-finite voxel, and the largest magnitude.
 struct BufStats {

@@ -348,6 +348,29 @@ hipError_t launch_interleave3(const float *a, const float *b, const float *c, fl
   return hipGetLastError();
 }
 
+// Channel sum of a multi-channel frame (vr_render_channels): out[e][i] = in[0][e][i] + in[1][e][i]
+// + ... in channel order, i.e. MATLAB's `main + structure` (example3.m:239) on the views' images
+// (nv views per channel, img floats each).
+__global__ void sum_channels_kernel(const float *__restrict__ in, uint32_t nch, uint32_t nv, uint64_t img,
+                                    float *__restrict__ out) {
+  const uint64_t n = img * nv;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = k / img, i = k - e * img;
+    float acc = in[e * img + i];
+    for (uint32_t c = 1; c < nch; ++c) acc = acc + in[((uint64_t)c * nv + e) * img + i];
+    out[k] = acc;
+  }
+}
+
+hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s) {
+  const uint64_t n = img * nv;
+  if (!n || !nch) return hipSuccess;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(sum_channels_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, nch, nv, img, out);
+  return hipGetLastError();
+}
+
 // Longest-first schedule of the march workgroups: order[] lists the tile blocks by
 // their last measured duration, longest first, in 256 log-spaced buckets (8 per octave; order
 // within a bucket is arbitrary).  The march writes the same image for any order.  One workgroup.

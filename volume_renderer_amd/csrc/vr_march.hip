@@ -495,6 +495,107 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
 }
 
 #if VR_MARCH_K <= 4
+// One wave's tile of workgroup `wg` of a view: ray setup, the march, the pixel store into `out` --
+// march_kernel's body for the multi-view launch below.  (march_kernel keeps its own copy: routed
+// through this function its register allocation changes, and the metric kernel is measured as is.)
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP>
+__device__ __forceinline__ void march_tile(const RenderParams &P, float *L, int lane, int wave, uint32_t wg,
+                                           int view, float *out, Ray &R, ChunkStats &C) {
+  using TS = TileShape<K>;
+  const int tile = (int)wg * VR_WG_WAVES + wave;
+  const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
+  const int blk = tile >> 2, quad = tile & 3;
+  const int ray = lane >> TS::LK;
+  const int lc = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + (ray / TS::TH);
+  const int y = (blk / nbx) * (2 * TS::TH) + (quad >> 1) * TS::TH + (ray % TS::TH);
+  const bool active = (lc < P.part_cols) && (y < P.height);
+  R.o = mk(0.f, 0.f, 0.f);
+  R.pos = R.o;
+  R.step = R.o;
+  R.t = 0.f;
+  R.tfar = -1.f;
+  R.sr = R.sg = R.sb = R.sa = 0.f;
+  R.nsteps = R.nlit = 0;
+  R.alive = false;
+  if (active) {
+    const int blk = lc / P.block_cols, within = lc - blk * P.block_cols;
+    const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
+    f3 d;
+    float tnear;
+    R.alive = ray_setup(P, x, y, R.o, d, tnear, R.tfar, view);
+    R.pos = mk(fmaf(d.x, tnear, R.o.x), fmaf(d.y, tnear, R.o.y), fmaf(d.z, tnear, R.o.z));
+    R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
+    R.t = tnear;
+  }
+  // every coordinate the march forms from a finite start and step is finite
+  if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
+  else
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
+
+  if (active && (lane & (K - 1)) == 0) {
+    const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
+    const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
+    out[kk] = R.sr;
+    out[kk + plane] = R.sg;
+    out[kk + 2 * plane] = R.sb;
+  }
+}
+
+// Fused views (vr_render_channels): the channels of a multi-channel frame, and of
+// each its stereo eyes, in one launch.  Every view has its own RenderParams (volumes, factors,
+// colour, lights, eye, output), all of them kernel arguments (scalar loads at a uniform offset;
+// pointers loaded from the argument segment stay global, which a device-memory table would lose),
+// and the same image and partition; view v marches workgroups [v * per_view, (v+1) * per_view).
+template <int K, int MODE, bool AB_ALIAS, int CAP>
+__global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, false)) void march_views_kernel(
+    const RenderViews V, uint32_t per_view) {
+  __shared__ float lds[VR_WG_WAVES][CAP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t view = blockIdx.x / per_view;
+  const RenderParams &P = V.p[view];
+  Ray R;
+  ChunkStats C{0, 0, 0, 0, 0};
+  march_tile<K, MODE, AB_ALIAS, false, false, false, CAP>(P, lds[wave], lane, wave, blockIdx.x - view * per_view, 0,
+                                                          P.out, R, C);
+}
+
+// Host entry (launch_march_views_k1 / _k2 / _k4): V.p[0 .. nviews) share the image, partition,
+// gradient mode (0 or 1), absorption aliasing and slot size; 32-bit addressing only.
+hipError_t VR_CAT(launch_march_views_k, VR_MARCH_K)(const RenderViews &V, uint32_t nviews, int mode, bool ab_alias,
+                                                   hipStream_t s) {
+  constexpr int K = VR_MARCH_K;
+  using TS = TileShape<K>;
+  const RenderParams &P0 = V.p[0];
+  if (nviews > VR_VIEWS_MAX) return hipErrorInvalidValue;
+  if (P0.part_cols <= 0 || P0.height <= 0 || nviews == 0) return hipSuccess;
+  if (mode > 1 || P0.steps || P0.wg_order) return hipErrorInvalidValue;
+  for (uint32_t v = 1; v < nviews; ++v)
+    if (V.p[v].part_cols != P0.part_cols || V.p[v].height != P0.height || V.p[v].wide_slot != P0.wide_slot)
+      return hipErrorInvalidValue;
+  const uint64_t tiles = (uint64_t)((P0.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
+                         (uint64_t)((P0.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
+  const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
+  if ((uint64_t)per_view * nviews > 0x7fffffffull) return hipErrorInvalidValue;
+  const dim3 grid(per_view * nviews), blk(64 * VR_WG_WAVES);
+#define VR_VIEWS_LAUNCH(M, A)                                                                                    \
+  do {                                                                                                           \
+    if (P0.wide_slot)                                                                                            \
+      hipLaunchKernelGGL((march_views_kernel<K, M, A, VR_LDS_CAP_WIDE>), grid, blk, 0, s, V, per_view);         \
+    else                                                                                                         \
+      hipLaunchKernelGGL((march_views_kernel<K, M, A, VR_LDS_CAP>), grid, blk, 0, s, V, per_view);              \
+  } while (0)
+  if (mode == 0) {
+    if (ab_alias) VR_VIEWS_LAUNCH(0, true);
+    else VR_VIEWS_LAUNCH(0, false);
+  } else {
+    if (ab_alias) VR_VIEWS_LAUNCH(1, true);
+    else VR_VIEWS_LAUNCH(1, false);
+  }
+#undef VR_VIEWS_LAUNCH
+  return hipGetLastError();
+}
+
 // Sort-last slab launch: one wave per 8x8 tile of the image part (the columns of
 // the image partition, vr_partition); per pixel the ray state (premultiplied r, g, b, alpha, and
 // 1 if the ray goes on past this slab) is read from P.slab_in (null: a fresh ray), marched

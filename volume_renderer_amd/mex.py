@@ -238,6 +238,50 @@ def gradient_device(d_data: int, dims, d_gx: int, d_gy: int, d_gz: int, stream: 
     _lib.check(_lib.lib().vr_gradient_device(d_data, dd, d_gx, d_gy, d_gz, stream))
 
 
+def channel(handle, t_sync, volumes, render_argv):
+    """One vr_channel: handle, the 'sync_volumes' arguments after the handle (t_sync, Emission,
+    Reflection, Absorption[, dx, dy, dz]) and the positional 'render' arguments after the handle.
+    Returns (VrChannel, keep-alive list)."""
+    c = _lib.VrChannel()
+    c.handle = _handle(handle)
+    c.time_last_mem_sync = int(np.asarray(t_sync).reshape(-1)[0])
+    vols = [_vr_volume(v) for v in volumes]
+    if len(vols) not in (3, 6):
+        raise _lib.VrError(5, "channel: expected 3 or 6 volumes")
+    c.emission, c.reflection, c.absorption = (ctypes.pointer(v) for v in vols[:3])
+    if len(vols) == 6:
+        c.dx, c.dy, c.dz = (ctypes.pointer(v) for v in vols[3:])
+    ra, keep = render_args(*render_argv)
+    c.args = ctypes.pointer(ra)
+    return c, [vols, ra, keep, [getattr(v, "Data", None) for v in volumes]]
+
+
+def render_channels(channels, stereo: bool = False, base: float = 0.0):
+    """Multi-channel frame (vr_render_channels): `channels` = [(handle, t_sync, volumes,
+    render_argv), ...]; returns one image (H, W, 3) per channel, or per channel a (left, right)
+    pair when stereo."""
+    built = [channel(*c) for c in channels]
+    arr = (_lib.VrChannel * len(built))(*[b[0] for b in built])
+    res = np.asarray(channels[0][3][4]).reshape(-1)
+    H, W = int(res[0]), int(res[1])
+    nv = 2 if stereo else 1
+    out = np.zeros((len(built) * nv, H * W * 3), dtype=np.float32)
+    check(lib().vr_render_channels(arr, len(built), 1 if stereo else 0, float(base),
+                                   out.ctypes.data_as(ctypes.c_void_p) if out.size else None))
+    del built
+    imgs = [out[k].reshape((H, W, 3), order="F") for k in range(out.shape[0])]
+    return [(imgs[2 * i], imgs[2 * i + 1]) for i in range(len(channels))] if stereo else imgs
+
+
+def render_channels_device(channels, d_out: int, stereo: bool = False, base: float = 0.0, stream: int = 0) -> None:
+    """vr_render_channels_device: channel i's view e into d_out + (i * eyes + e) * H*W*3 floats."""
+    built = [channel(*c) for c in channels]
+    arr = (_lib.VrChannel * len(built))(*[b[0] for b in built])
+    check(lib().vr_render_channels_device(arr, len(built), 1 if stereo else 0, float(base),
+                                          ctypes.c_void_p(int(d_out)), ctypes.c_void_p(int(stream)) if stream else None))
+    del built
+
+
 def volumeRender(cmd, *args):
     """The `volumeRender` mex: commands 'new', 'delete', 'mem_info', 'sync_volumes', 'render'."""
     nrhs = 1 + len(args)
@@ -248,6 +292,8 @@ def volumeRender(cmd, *args):
         p = ctypes.c_void_p()
         check(L.vr_new(ctypes.byref(p)))
         return np.uint64(p.value)
+    if cmd == "render_channels":  # vr_render_channels: ('render_channels', channels[, stereo, base])
+        return render_channels(*args)
     if nrhs < 2:
         raise _lib.VrError(1, "Second input should be a class instance handle.")
     h = _handle(args[0])

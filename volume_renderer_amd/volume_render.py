@@ -149,21 +149,29 @@ class VolumeRender:
         self.VolumeGradientY = False
         self.VolumeGradientZ = False
 
+    def _stereo_geometry(self):
+        """VolumeRender.m:278-283: (base, delta, resolution [H W+delta]) of the stereo pair."""
+        base = self.CameraXOffset / 2
+        fov = 2 * math.atan(1 / self.FocalLength)
+        delta = base * self.ImageResolution[1] / (2 * self.FocalLength * math.tan(fov / 2))
+        delta = int(math.floor(abs(delta) + 0.5)) * (1 if delta >= 0 else -1)  # MATLAB round
+        return base, delta, np.flip(self.ImageResolution) + np.array([0, delta])
+
     def render(self) -> np.ndarray:
         """VolumeRender.m:264-309: mono render, or off-axis stereo composed from two renders."""
         res = np.flip(self.ImageResolution)  # [H W]
         if self.CameraXOffset == 0:
             return self._p_render(np.float32(self.CameraXOffset), res)
-        base = self.CameraXOffset / 2
-        fov = 2 * math.atan(1 / self.FocalLength)
-        delta = base * self.ImageResolution[1] / (2 * self.FocalLength * math.tan(fov / 2))
-        delta = int(math.floor(abs(delta) + 0.5)) * (1 if delta >= 0 else -1)  # MATLAB round
-        resolution = res + np.array([0, delta])
+        base, delta, resolution = self._stereo_geometry()
         if os.environ.get("VR_NO_FUSED_STEREO") == "1":  # the reference's two renders
             right = self._p_render(base, resolution)
             left = self._p_render(-base, resolution)
         else:  # both eyes in one launch (vr_render_stereo), the same images
             left, right = self._p_render(np.float32(base), resolution, stereo=True)
+        return self._compose(left, right, delta)
+
+    def _compose(self, left, right, delta):
+        """VolumeRender.m:288-307: crop the eyes, red-cyan anaglyph or side by side."""
         left = _imcrop(left, delta + 1, left.shape[1])
         right = _imcrop(right, 0, right.shape[1] - delta)
         if self.StereoOutput == StereoRenderMode.RedCyan:
@@ -173,6 +181,62 @@ class VolumeRender:
             img[:, :, 2] = right[:, :, 2]
             return img
         return np.asfortranarray(np.concatenate([left, right], axis=1))
+
+    @staticmethod
+    def renderChannels(renders) -> list:
+        """The channels of a multi-channel frame (examples/example3.m: one VolumeRender per
+        channel, images added afterwards), marched together (vr_render_channels): per channel the
+        image its render() returns.  The channels need distinct objects and equal ImageResolution,
+        CameraXOffset and FocalLength."""
+        r0 = renders[0]
+        for r in renders[1:]:
+            if (list(r.ImageResolution) != list(r0.ImageResolution) or r.CameraXOffset != r0.CameraXOffset
+                    or (r0.CameraXOffset != 0 and r.FocalLength != r0.FocalLength)):
+                raise ValueError("channels differ in ImageResolution / CameraXOffset / FocalLength")
+        stereo = r0.CameraXOffset != 0
+        if stereo:
+            base, delta, resolution = r0._stereo_geometry()
+        else:
+            base, delta, resolution = 0.0, 0, np.flip(r0.ImageResolution)
+        chans = []
+        for r in renders:
+            with_grads = r._validate_volumes()
+            argv = r._render_argv(np.float32(-base if stereo else 0.0), resolution)
+            vols = [r.VolumeEmission, r.VolumeReflection, r.VolumeAbsorption]
+            if with_grads:
+                vols += [r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ]
+            chans.append((r.objectHandle, r.TimeLastMemSync, vols, argv))
+        out = volumeRender("render_channels", chans, stereo, np.float32(base))
+        for r in renders:  # each channel was synced (syncVolumes, VolumeRender.m:188-219)
+            r.TimeLastMemSync = timestamp()
+        if not stereo:
+            return list(out)
+        return [r._compose(left, right, delta) for r, (left, right) in zip(renders, out)]
+
+    def _validate_volumes(self) -> bool:
+        """VolumeRender.m:497-520: volumes set; returns whether gradient volumes are used."""
+        validate = [_is_logical(self.VolumeReflection), _is_logical(self.VolumeAbsorption),
+                    _is_logical(self.VolumeEmission)]
+        if _is_logical(self.VolumeIllumination):
+            warnings.warn("VolumeIllumination is unset. Thus no lightning will be applied!")
+        if any(validate):
+            raise ValueError("Not all volumes are properly set!")
+        grads = [self.VolumeGradientX, self.VolumeGradientY, self.VolumeGradientZ]
+        if not any(_is_logical(g) for g in grads):
+            if not all(isinstance(g, Volume) for g in grads):
+                raise ValueError("All gradient dimensions need to be set and of type Volume!")
+            return True
+        return False
+
+    def _render_argv(self, camera_x_offset, resolution) -> list:
+        """The positional 'render' arguments after the handle (VolumeRender.m:560-575)."""
+        factors = np.array([self.FactorEmission, self.FactorReflection, self.FactorAbsorption])
+        props = np.array([camera_x_offset, self.FocalLength, self.DistanceToObject], dtype=np.float64)
+        matrix = np.flip(self.RotationMatrix, axis=0)
+        return [self.LightSources, self.VolumeIllumination, factors.astype(np.float32),
+                self.ElementSizeUm.astype(np.float32), np.asarray(resolution).astype(np.uint64),
+                matrix.astype(np.float32), props.astype(np.float32), np.float32(self.OpacityThreshold),
+                self.Color.astype(np.float32)]
 
     def _p_render(self, camera_x_offset, resolution, stereo=False):
         """VolumeRender.m:497-583 (stereo=True: both eyes at +-camera_x_offset, one launch)."""
