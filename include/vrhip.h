@@ -126,8 +126,11 @@ int vr_render_stereo(vr_context *h, const vr_render_args *args, float base, floa
  * 61-233 -- sync a channel's volumes, render, next channel -- and the sum at example3.m:239).  A
  * channel is one VolumeRender object: its handle (distinct per channel), the arguments of its
  * 'sync_volumes' (volumeRender.cpp:600-633; dx/dy/dz NULL = on-the-fly gradient) and of its
- * 'render'.  Channel i equals vr_sync_volumes + vr_render on it, in channel order (stereo != 0:
- * vr_render_stereo with `base`, left then right); every channel must have the same resolution.
+ * 'render'.  Channel i equals vr_sync_volumes + vr_render on it (stereo != 0: vr_render_stereo
+ * with `base`, left then right) were its handle the only one: before the channel's sync, the
+ * texture bindings its handle's last sync left are restored (the reference's textures are module
+ * globals, kernel.cu:49-120, so with one object per channel an unchanged channel would render the
+ * previous channel's volumes).  Every channel must have the same resolution.
  * The channels' frames are marched together (one launch per gradient-mode / absorption / shading
  * group).  vr_render_channels writes channel i's view e (e = 0 left / only, 1 right; eyes = 1 or
  * 2) to out[(i * eyes + e) * H*W*3 ...], each laid out as vr_render's image; the caller adds them

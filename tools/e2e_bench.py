@@ -91,6 +91,29 @@ def main():
 
     out["stereo_two_renders_ms"] = round(med(two_renders), 2)
     out["stereo_fused_ms"] = round(med(lambda: vr.volumeRender("render_stereo", *scall[1:], np.float32(base))), 2)
+    # two channels x stereo (BASELINE C4 shape, examples/example3.m): a structure channel with its
+    # own object (colour [0 1 0], Fe 0.5) beside the main one; per channel a fused stereo render
+    # vs all four views in one vr_render_channels launch
+    em2 = vr.Volume(host)
+    h2 = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h2, np.uint64(0), em2, refl, em2)
+    t_last2 = np.uint64(mex.timestamp())
+    c2 = list(scall)
+    c2[1] = h2
+    c2[4] = np.float32([0.5, 0.4, 1.0])
+    c2[10] = np.float32([0, 1, 0])
+
+    def per_channel():
+        vr.volumeRender("sync_volumes", h, t_last, em, refl, em)
+        vr.volumeRender("render_stereo", *scall[1:], np.float32(base))
+        vr.volumeRender("sync_volumes", h2, t_last2, em2, refl, em2)
+        vr.volumeRender("render_stereo", *c2[1:], np.float32(base))
+
+    chans = [(h, t_last, [em, refl, em], scall[2:]), (h2, t_last2, [em2, refl, em2], c2[2:])]
+    out["channels2_stereo_per_channel_ms"] = round(med(per_channel), 2)
+    out["channels2_stereo_fused_ms"] = round(med(lambda: mex.render_channels(chans, True, np.float32(base))), 2)
+    vr.volumeRender("delete", h2)  # resets every handle (cudaDeviceReset): re-sync the main one
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)
     if not args.no_lookup:
         grads = em.grad() if n <= 256 else _device_grad(host, mex, vr)
         t0 = time.perf_counter()

@@ -174,6 +174,12 @@ struct vr_context {
   std::vector<unsigned char> h_views;  // host image of d_views (alive until the copy has run)
   float *d_chan = nullptr;             // per-view images of the host entry
   size_t d_chan_bytes = 0;
+  // the module-global texture bindings as this handle's last sync left them (vr_render_channels
+  // restores them before the channel's sync); weak: they never keep a buffer alive
+  std::weak_ptr<DevBuf> snap_bind[T_COUNT];
+  int32_t snap_idx[3] = {0, 0, 0};
+  int32_t snap_grad = 0;
+  bool has_snap = false;
 };
 
 namespace {
@@ -1050,6 +1056,12 @@ static int do_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_
   g_tex.grad_method = lookup ? G_LOOKUP : G_COMPUTE;  // setGradientMethod (render.cpp:121)
   mm_sync(h);
   VR_HIP(hipDeviceSynchronize());
+  for (int t = 0; t < T_COUNT; ++t) h->snap_bind[t] = g_tex.bind[t];
+  h->snap_idx[0] = g_tex.idx_em;
+  h->snap_idx[1] = g_tex.idx_ab;
+  h->snap_idx[2] = g_tex.idx_re;
+  h->snap_grad = g_tex.grad_method;
+  h->has_snap = true;
   return VR_OK;
   VR_GUARD_END
 }
@@ -1062,8 +1074,11 @@ int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume 
 }
 
 // Multi-channel render (vr_render_channels): channel i is what vr_sync_volumes +
-// vr_render (or vr_render_stereo) on ch[i] in channel order would produce -- the syncs run in that
-// order, each channel's frame is prepared against the textures its own sync bound, and the frames
+// vr_render (or vr_render_stereo) on ch[i] would produce were it the only object -- before its
+// sync the texture bindings its handle's last sync left are restored (the reference's textures are
+// module globals: with one object per channel an unchanged channel would otherwise render the
+// previous channel's volumes); the syncs run in channel order, each channel's frame is prepared
+// against the textures its own sync bound, and the frames
 // the staged march can take are marched together in one launch per (gradient mode, absorption
 // aliasing, slot size, shading) group, their views' parameters in device memory.  The buffers a
 // prepared frame reads stay referenced until the call returns; a later channel's sync never
@@ -1093,6 +1108,13 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
   std::vector<size_t> loff;
   for (int i = 0; i < n; ++i) {
     vr_context *h = ch[i].handle;
+    if (h->has_snap) {  // this channel's own bindings, not the previous channel's
+      for (int t = 0; t < T_COUNT; ++t) g_tex.bind[t] = h->snap_bind[t].lock();
+      g_tex.idx_em = h->snap_idx[0];
+      g_tex.idx_ab = h->snap_idx[1];
+      g_tex.idx_re = h->snap_idx[2];
+      g_tex.grad_method = h->snap_grad;
+    }
     int rc = do_sync_volumes(h, ch[i].time_last_mem_sync, ch[i].emission, ch[i].reflection, ch[i].absorption,
                              ch[i].dx, ch[i].dy, ch[i].dz);
     if (rc) return rc;
@@ -1160,9 +1182,9 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
   while (g0 < nvw) {
     size_t g1 = g0;
     while (g1 < nvw && key(order[g1]) == key(order[g0])) ++g1;
-    vr::RenderParams T = views[order[g0]];
-    T.height *= (int32_t)(g1 - g0);  // the group's waves decide the depth lanes
-    const int K = std::min(depth_lanes(T), 4);
+    // depth lanes as for one view: the frame's own tail sets them, and K = 2 stays ahead of K = 1
+    // per sample even at many waves per slot
+    const int K = std::min(depth_lanes(views[order[g0]]), 4);
     vr::RenderViews V;
     std::memset(&V, 0, sizeof V);
     for (size_t k = g0; k < g1; ++k) {
