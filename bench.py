@@ -36,6 +36,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 METRIC = "Mrays/s + achieved HBM GB/s, 1024³ vol @ 1920×1080 HG-shaded, 1/2/4/8 GPU"
 
 
+def workload_name(n, W, H, L, gradient):
+    """config.workload; also the key profiles/<round>/traffic.json must carry for roofline.traffic."""
+    return (f"V_shell({n}) fp32 {n}^3, {W}x{H}, "
+            + ("HG 2 lights (example1.m), on-the-fly gradient" if (L == 2 and gradient == "compute")
+               else f"HG {L} lights, {gradient} gradient (diagnostic)")
+            + ", rotate(125,25,0) f=3 dist=6 thr=0.9")
+
+
 def rotation(alpha, beta, gamma):
     """VolumeRender.rotate from identity (exact cosd/sind at multiples of 90)."""
     from volume_renderer_amd.volume_render import _cosd, _sind
@@ -265,11 +273,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic V_shell(%d) (SURVEY.md 8d), generated in HBM" % n,
-            "config": {"workload": f"V_shell({n}) fp32 {n}^3, {W}x{H}, "
-                                   + ("HG 2 lights (example1.m), on-the-fly gradient"
-                                      if (L == 2 and args.gradient == "compute") else
-                                      f"HG {L} lights, {args.gradient} gradient (diagnostic)")
-                                   + ", rotate(125,25,0) f=3 dist=6 thr=0.9",
+            "config": {"workload": workload_name(n, W, H, L, args.gradient),
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else ""),

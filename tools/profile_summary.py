@@ -6,7 +6,9 @@ traffic.json (HBM bytes per launch of the march kernel, read by bench.py for roo
 HBM bytes: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B per 128 B request
 (MI355X_MICROARCH.md, HBM section), so read bytes = 2 x 1024 x FETCH_SIZE.  The factor is checked
 here on stats_kernel, which reads every padded voxel once (known byte count).
-usage: tools/profile_summary.py gpurun_out/r13 profiles/round1 WORKLOAD_STRING"""
+usage: tools/profile_summary.py gpurun_out/r13 profiles/round1 [WORKLOAD_STRING]
+The workload key defaults to the bench.json line of the run (bench.py matches it verbatim against
+its config.workload before it reports roofline.traffic)."""
 import csv
 import glob
 import json
@@ -16,7 +18,11 @@ import shutil
 import sys
 from collections import defaultdict
 
-run, out, workload = sys.argv[1], sys.argv[2], sys.argv[3]
+run, out = sys.argv[1], sys.argv[2]
+workload = sys.argv[3] if len(sys.argv) > 3 else None
+if workload is None:
+    with open(os.path.join(run, "bench.json")) as fh:
+        workload = json.loads(fh.read().strip().splitlines()[-1])["config"]["workload"]
 os.makedirs(out, exist_ok=True)
 ks = glob.glob(os.path.join(run, "kt", "*kernel_stats.csv"))
 if ks:
