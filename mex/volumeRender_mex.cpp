@@ -3,8 +3,7 @@
 // VolumeRender.m / Volume.m / LightSource.m run unchanged on MI355X.
 //
 // Not built in this repository (it needs MATLAB's mex.h / libmx); a maintainer builds it with
-//   mex -R2018a -I<repo>/include -L<repo>/volume_renderer_amd -lvrhip volumeRender_mex.cpp \
-//       -output volumeRender
+//   mex -R2018a -I<repo>/include -L<repo>/volume_renderer_amd -lvrhip volumeRender_mex.cpp -output volumeRender
 // and puts the result where src/make.m put the CUDA mex (src/matlab/VolumeRender/).  See
 // INTEGRATION.md.  All marshalling permutations (reversed ElementSizeUm and light positions,
 // flip(R) un-flipping, [H W] order) happen inside libvrhip exactly as the reference's mex did them;
@@ -57,6 +56,86 @@ const T *data_of(const mxArray *a, size_t n, const char *what) {
   return static_cast<const T *>(mxGetData(a));
 }
 
+// The 'render' arguments Lights, Illum, factors, ElementSizeUm, [H W], flip(R), props, thr, Color
+// (render.cpp:134-221), p[0] = Lights.  `lights` / `illum` own what a.lights / a.illumination point to.
+void unpack_render(const mxArray *const *p, vr_render_args &a, std::vector<vr_light> &lights, vr_volume &illum) {
+  a = vr_render_args{};
+  const bool lit = !(mxIsClass(p[0], "logical") || mxIsClass(p[1], "logical"));
+  if (lit) {
+    const size_t n = mxGetN(p[0]);
+    lights.resize(n);
+    for (size_t l = 0; l < n; ++l) {
+      const float *pos = static_cast<const float *>(mxGetData(mxGetProperty(p[0], l, "Position")));
+      const float *col = static_cast<const float *>(mxGetData(mxGetProperty(p[0], l, "Color")));
+      memcpy(lights[l].position, pos, sizeof(lights[l].position));
+      memcpy(lights[l].color, col, sizeof(lights[l].color));
+    }
+    illum = make_volume(p[1]);
+    a.lights = lights.data();
+    a.num_lights = (int64_t)n;
+    a.illumination = &illum;
+  } else {
+    a.num_lights = -1;  // the logical `false`
+    a.illumination = nullptr;
+  }
+  memcpy(a.factors, data_of<float>(p[2], 3, "factors: 3 singles expected"), sizeof(a.factors));
+  memcpy(a.element_size_um, data_of<float>(p[3], 3, "ElementSizeUm: 3 singles expected"),
+         sizeof(a.element_size_um));
+  memcpy(a.resolution, data_of<uint64_t>(p[4], 2, "resolution: uint64 [H W] expected"), sizeof(a.resolution));
+  memcpy(a.rotation_flipped, data_of<float>(p[5], 9, "rotation: 3x3 single expected"), sizeof(a.rotation_flipped));
+  memcpy(a.props, data_of<float>(p[6], 3, "properties: 3 singles expected"), sizeof(a.props));
+  a.opacity_threshold = (float)mxGetScalar(p[7]);
+  memcpy(a.color, data_of<float>(p[8], 3, "Color: 3 singles expected"), sizeof(a.color));
+}
+
+mxArray *new_image(const vr_render_args &a, mwSize views) {
+  const mwSize dim[4] = {(mwSize)a.resolution[0], (mwSize)a.resolution[1], 3, views};
+  return mxCreateNumericArray(views > 1 ? 4 : 3, dim, mxSINGLE_CLASS, mxREAL);
+}
+
+// volumeRender('render_channels', {ch1, ch2, ...}, stereo, base) -> single [H W 3 n*eyes]
+// (vr_render_channels; examples/example3.m:61-239 as one call).  A channel is a cell
+// {h, TimeLastMemSync, Em, Re, Ab, Lights, Illum, factors, ElementSizeUm, [H W], flip(R), props,
+// thr, Color} -- the arguments of its 'sync_volumes' and 'render' -- optionally followed by
+// Gx, Gy, Gz (gradient lookup).  Page (i * eyes + e) is channel i's view e; MATLAB adds them.
+void render_channels(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
+  if (nlhs > 1) mexErrMsgTxt("Too many output arguments.");
+  if (nrhs < 4 || !mxIsCell(prhs[1])) mexErrMsgTxt("render_channels: {channels}, stereo, base expected");
+  const mwSize n = mxGetNumberOfElements(prhs[1]);
+  if (n == 0) mexErrMsgTxt("render_channels: no channels");
+  const int32_t stereo = mxGetScalar(prhs[2]) != 0.0;
+  const float base = (float)mxGetScalar(prhs[3]);
+  std::vector<vr_volume> vols(6 * n);
+  std::vector<vr_render_args> args(n);
+  std::vector<std::vector<vr_light>> lights(n);
+  std::vector<vr_volume> illum(n);
+  std::vector<vr_channel> ch(n);
+  for (mwSize i = 0; i < n; ++i) {
+    const mxArray *c = mxGetCell(prhs[1], i);
+    const mwSize m = c && mxIsCell(c) ? mxGetNumberOfElements(c) : 0;
+    if (m != 14 && m != 17) mexErrMsgTxt("render_channels: a channel is a cell of 14 or 17 elements");
+    const mxArray *e[17];
+    for (mwSize k = 0; k < m; ++k) e[k] = mxGetCell(c, k);
+    ch[i].handle = handle(e[0]);
+    ch[i].time_last_mem_sync = (uint64_t)mxGetScalar(e[1]);
+    for (int k = 0; k < 3; ++k) vols[6 * i + k] = make_volume(e[2 + k]);
+    ch[i].emission = &vols[6 * i];
+    ch[i].reflection = &vols[6 * i + 1];
+    ch[i].absorption = &vols[6 * i + 2];
+    if (m == 17) {
+      for (int k = 0; k < 3; ++k) vols[6 * i + 3 + k] = make_volume(e[14 + k]);
+      ch[i].dx = &vols[6 * i + 3];
+      ch[i].dy = &vols[6 * i + 4];
+      ch[i].dz = &vols[6 * i + 5];
+    }
+    unpack_render(e + 5, args[i], lights[i], illum[i]);
+    ch[i].args = &args[i];
+  }
+  mxArray *img = new_image(args[0], n * (stereo ? 2 : 1));
+  check(vr_render_channels(ch.data(), (int32_t)n, stereo, base, static_cast<float *>(mxGetData(img))));
+  plhs[0] = img;
+}
+
 }  // namespace
 
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
@@ -72,6 +151,10 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     mexLock();  // the module-global device state must outlive `clear functions`
     plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
     *static_cast<uint64_t *>(mxGetData(plhs[0])) = reinterpret_cast<uint64_t>(h);
+    return;
+  }
+  if (!strcmp(cmd, "render_channels")) {
+    render_channels(nlhs, plhs, nrhs, prhs);
     return;
   }
   if (nrhs < 2) mexErrMsgTxt("Second input should be a class instance handle.");
@@ -102,43 +185,27 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     if (nlhs != 0 || nrhs > 9) mexWarnMsgTxt("SyncVolumes: Unexpected arguments ignored.");
     return;
   }
-  if (!strcmp(cmd, "render")) {
-    if (nlhs > 1) mexErrMsgTxt("Too many output arguments.");
-    if (nrhs < 11) mexErrMsgTxt("insufficient parameter!");
-    vr_render_args a{};
+  if (!strcmp(cmd, "render") || !strcmp(cmd, "render_stereo")) {
+    const bool stereo = cmd[6] != '\0';
+    if (nlhs > (stereo ? 2 : 1)) mexErrMsgTxt("Too many output arguments.");
+    if (nrhs < (stereo ? 12 : 11)) mexErrMsgTxt("insufficient parameter!");
+    vr_render_args a;
     std::vector<vr_light> lights;
     vr_volume illum{};
-    const bool lit = !(mxIsClass(prhs[2], "logical") || mxIsClass(prhs[3], "logical"));
-    if (lit) {
-      const size_t n = mxGetN(prhs[2]);
-      lights.resize(n);
-      for (size_t l = 0; l < n; ++l) {
-        const float *pos = static_cast<const float *>(mxGetData(mxGetProperty(prhs[2], l, "Position")));
-        const float *col = static_cast<const float *>(mxGetData(mxGetProperty(prhs[2], l, "Color")));
-        memcpy(lights[l].position, pos, sizeof(lights[l].position));
-        memcpy(lights[l].color, col, sizeof(lights[l].color));
-      }
-      illum = make_volume(prhs[3]);
-      a.lights = lights.data();
-      a.num_lights = (int64_t)n;
-      a.illumination = &illum;
-    } else {
-      a.num_lights = -1;  // the logical `false`
-      a.illumination = nullptr;
+    unpack_render(prhs + 2, a, lights, illum);
+    if (!stereo) {
+      mxArray *img = new_image(a, 1);
+      check(vr_render(h, &a, static_cast<float *>(mxGetData(img))));
+      plhs[0] = img;
+      return;
     }
-    memcpy(a.factors, data_of<float>(prhs[4], 3, "factors: 3 singles expected"), sizeof(a.factors));
-    memcpy(a.element_size_um, data_of<float>(prhs[5], 3, "ElementSizeUm: 3 singles expected"),
-           sizeof(a.element_size_um));
-    memcpy(a.resolution, data_of<uint64_t>(prhs[6], 2, "resolution: uint64 [H W] expected"), sizeof(a.resolution));
-    memcpy(a.rotation_flipped, data_of<float>(prhs[7], 9, "rotation: 3x3 single expected"),
-           sizeof(a.rotation_flipped));
-    memcpy(a.props, data_of<float>(prhs[8], 3, "properties: 3 singles expected"), sizeof(a.props));
-    a.opacity_threshold = (float)mxGetScalar(prhs[9]);
-    memcpy(a.color, data_of<float>(prhs[10], 3, "Color: 3 singles expected"), sizeof(a.color));
-    const mwSize dim[3] = {(mwSize)a.resolution[0], (mwSize)a.resolution[1], 3};
-    mxArray *img = mxCreateNumericArray(3, dim, mxSINGLE_CLASS, mxREAL);
-    check(vr_render(h, &a, static_cast<float *>(mxGetData(img))));
-    plhs[0] = img;
+    // volumeRender('render_stereo', h, <render args>, base) -> [left, right] (vr_render_stereo;
+    // VolumeRender.m:278-307's two renders at camera offsets -base / +base in one launch)
+    mxArray *left = new_image(a, 1), *right = new_image(a, 1);
+    check(vr_render_stereo(h, &a, (float)mxGetScalar(prhs[11]), static_cast<float *>(mxGetData(left)),
+                           static_cast<float *>(mxGetData(right))));
+    plhs[0] = left;
+    if (nlhs > 1) plhs[1] = right; else mxDestroyArray(right);
     return;
   }
   mexErrMsgTxt(("Unknown command: " + std::string(cmd)).c_str());
