@@ -579,3 +579,47 @@ def test_channels_mixed_gradient_modes(monkeypatch, counter_clock):
     for a, b in zip(sep, fused):
         assert a.max() > 0
         assert np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_channels_device_images_and_fp32_sum(counter_clock):
+    """vr_render_channels_device writes each channel's image where the host variant returns it, bit
+    for bit; vr_sum_channels_device adds them in channel order in fp32 (the channel sum of
+    examples/example3.m:239, kept on the device)."""
+    import torch
+    from volume_renderer_amd import mex
+
+    def three():
+        main, struct = _channel_pair(True)
+        third = ex1_renderer(vr.Volume(O.shell_volume(40)), res=(90, 70), lights=True)
+        third.Color = [1, 0, 0]
+        third.FactorEmission = 0.25
+        return main, struct, third
+
+    def chans(rs):
+        out = []
+        for r in rs:
+            r._validate_volumes()
+            argv = r._render_argv(np.float32(0.0), np.flip(r.ImageResolution))
+            out.append((r.objectHandle, r.TimeLastMemSync,
+                        [r.VolumeEmission, r.VolumeReflection, r.VolumeAbsorption], argv))
+        return out
+
+    hr = three()
+    host = mex.render_channels(chans(hr))
+    dr = three()
+    n = host[0].size
+    d = torch.zeros(3 * n, dtype=torch.float32, device="cuda")
+    s = torch.zeros(n, dtype=torch.float32, device="cuda")
+    mex.render_channels_device(chans(dr), d.data_ptr())
+    mex.sum_channels_device(d.data_ptr(), 3, 1, n, s.data_ptr())
+    torch.cuda.synchronize()
+    dev = d.cpu().numpy().reshape(3, n)
+    flat = [np.asarray(h, np.float32).reshape(-1, order="F") for h in host]
+    for i in range(3):
+        assert flat[i].max() > 0
+        assert np.array_equal(dev[i].view(np.uint32), flat[i].view(np.uint32))
+    want = (flat[0] + flat[1]) + flat[2]
+    assert np.array_equal(s.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    for r in hr + dr:
+        r.delete()

@@ -282,6 +282,12 @@ def render_channels_device(channels, d_out: int, stereo: bool = False, base: flo
     del built
 
 
+def sum_channels_device(d_in: int, n: int, views: int, image_floats: int, d_out: int, stream: int = 0) -> None:
+    """vr_sum_channels_device: d_out[e] = d_in[0][e] + d_in[1][e] + ... (fp32, channel order)."""
+    check(lib().vr_sum_channels_device(ctypes.c_void_p(int(d_in)), int(n), int(views), int(image_floats),
+                                       ctypes.c_void_p(int(d_out)), ctypes.c_void_p(int(stream)) if stream else None))
+
+
 def volumeRender(cmd, *args):
     """The `volumeRender` mex: commands 'new', 'delete', 'mem_info', 'sync_volumes', 'render'."""
     nrhs = 1 + len(args)
