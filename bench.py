@@ -9,11 +9,11 @@ threshold 0.9, camera rotate(125,25,0), f=3, dist=6, reflection = the class defa
 A "step" = one frame: the ray-march kernel over this rank's image columns (+ at N>1 the RCCL
 gather of the column partitions to rank 0 and the on-device assembly of the full image).
 Volumes are resident in HBM before the timed region (sync_volumes is not timed).  The K timed
-frames are independent (a movie, examples/example3.m) and are issued round-robin on --streams HIP
-streams (default 2), each with its own output buffers, so that one frame's tail -- its longest
-waves -- overlaps the next frame's start; `value` / `ms_per_step` are that throughput.  A serial
-pass of K frames (one after the other) runs first: its HIP-event kernel times give
-roofline.kernel_ms / achieved, and its wall time is `serial_ms_per_step`.
+frames run one after the other on one HIP stream -- what a synchronous VolumeRender.render user
+gets per frame (minus the D2H copy) -- so `value` / `ms_per_step` are the serial frame rate and
+`ms_per_step` >= the march kernel's own time.  A second, separately reported pass
+(`pipelined`, --pipelined-streams, default 2) issues independent frames of a movie round-robin on
+several streams so that one frame's tail overlaps the next frame's start; it is not `value`.
 Run: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
 """
 from __future__ import annotations
@@ -33,6 +33,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD at 2.4 GHz
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
+VALU_ISSUE_PER_S = 1024 * 2.4e9 / 2
 METRIC = "Mrays/s + achieved HBM GB/s, 1024³ vol @ 1920×1080 HG-shaded, 1/2/4/8 GPU"
 
 
@@ -64,7 +67,9 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--block-cols", type=int, default=16, help="column block of the image partition")
     ap.add_argument("--cpu-stride", type=int, default=8, help="CPU baseline: every k-th column")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
+    ap.add_argument("--cpu-stride-1core", type=int, default=96, help="1-core CPU baseline: every k-th column")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every CPU this process may use -- affinity and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gradient", choices=["compute", "lookup"], default="compute",
                     help="lookup: precomputed gradient volumes (example1_grad.m, BASELINE config 3), made on "
@@ -74,12 +79,10 @@ def main():
     ap.add_argument("--sim-parts", type=int, default=0,
                     help="diagnostic (1 GPU): also time each rank's share of a P-way column partition, "
                          "the kernel time a rank would see at --gpus P")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams the timed frames are issued on round-robin: frames are independent (a "
-                         "movie, example3.m), so one frame's tail -- its longest waves -- overlaps the next "
-                         "frame's start.  1: strictly one frame after the other.  The kernel time of the "
-                         "roofline always comes from a serial pass.")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "round1", "traffic.json"),
+    ap.add_argument("--pipelined-streams", type=int, default=2,
+                    help="extra pass (not `value`): the frames issued round-robin on this many HIP streams "
+                         "(independent frames of a movie, example3.m); 1 or 0 skips it")
+    ap.add_argument("--traffic-json", default=_latest_traffic_json(),
                     help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
 
@@ -180,9 +183,10 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
 
-    serial_elapsed = elapsed
-    if args.streams > 1:
-        ns = args.streams
+    # ---- extra pass (not `value`): independent frames round-robin on several streams ----------
+    pipe_elapsed = None
+    ns = args.pipelined_streams
+    if ns > 1:
         streams = [torch.cuda.Stream(dev) for _ in range(ns)]
         outs = [torch.zeros_like(out_local) for _ in range(ns)]
         fulls = [torch.zeros(3 * W * H, dtype=torch.float32, device=dev) for _ in range(ns)] if rank == 0 else None
@@ -212,7 +216,8 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        elapsed = time.perf_counter() - t1
+        pipe_elapsed = time.perf_counter() - t1
+        del outs, fulls, gaths
 
     sim = None
     if args.sim_parts > 1 and world == 1:
@@ -230,24 +235,14 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize(dev)
             sim.append(round(e0.elapsed_time(e1) / 3, 3))
-            if args.streams > 1:  # the same share, launches alternating over streams
-                ss = [torch.cuda.Stream(dev) for _ in range(args.streams)]
-                for k in range(2 * len(ss)):  # each stream's first launch measures its schedule
-                    mex.render_device(h, ra, sim_out.data_ptr(), pp, 0, ss[k % len(ss)].cuda_stream)
-                torch.cuda.synchronize(dev)
-                t2 = time.perf_counter()
-                for k in range(6):
-                    mex.render_device(h, ra, sim_out.data_ptr(), pp, 0, ss[k % len(ss)].cuda_stream)
-                torch.cuda.synchronize(dev)
-                sim[-1] = (sim[-1], round((time.perf_counter() - t2) / 6 * 1e3, 3))
         del sim_out
 
     samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=dev)
-    el = torch.tensor([elapsed, serial_elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed, pipe_elapsed or 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(samples_all, op=dist.ReduceOp.SUM)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed, serial_elapsed = float(el[0].item()), float(el[1].item())
+    elapsed, pipe_elapsed = float(el[0].item()), (float(el[1].item()) if pipe_elapsed is not None else None)
     total_samples = int(samples_all[0].item())
     total_lit = int(samples_all[1].item())
 
@@ -260,6 +255,9 @@ def main():
         F = 1 + ((G + 1 + L) if L > 0 else 0)  # trilinear fetches per sample, SURVEY.md 8d
         bytes_launch = 4.0 * my_samples * F + 12.0 * my_cols * H
         achieved = bytes_launch / t_kernel_s / 1e9
+        # the fetches a sample really needs: every sample its centre fetch, only the shaded ones the
+        # F - 1 gradient / reflection / LUT fetches (opacity-0 samples add exactly 0)
+        fetched = 4.0 * (my_samples + my_lit * (F - 1)) + 12.0 * my_cols * H
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -277,7 +275,8 @@ def main():
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else ""),
-                       "depth_lanes": mex.depth_lanes(my_cols, H)},
+                       "depth_lanes": mex.depth_lanes(my_cols, H),
+                       "frames": "serial, one HIP stream"},
             "samples_per_frame": total_samples,
             "shaded_samples_per_frame": total_lit,
             "chunks_staged_leaped_global": chunk_stats,
@@ -289,66 +288,135 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel_ms": round(t_kernel_s * 1e3, 3),
                          "bytes_per_launch": bytes_launch,
-                         "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F},
+                         "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F,
+                         "fetched": {"bytes_per_launch": fetched,
+                                     "achieved": round(fetched / t_kernel_s / 1e9, 1),
+                                     "frac": round(fetched / t_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                                     "what": "4 B x (samples + shaded samples x (F-1)) + 12 B x pixels"},
+                         "valu": None},
             "cpu_baseline": None,
         }
-        result["streams"] = args.streams
-        result["serial_ms_per_step"] = round(serial_elapsed / args.steps * 1e3, 3)
+        if pipe_elapsed is not None:
+            result["pipelined"] = {"streams": ns, "ms_per_step": round(pipe_elapsed / args.steps * 1e3, 3),
+                                   "mrays_s": round(rays * args.steps / pipe_elapsed / 1e6, 3),
+                                   "what": "the same frames issued round-robin on several HIP streams "
+                                           "(independent movie frames overlap their tails); not `value`"}
         if sim is not None:
-            if args.streams > 1:
-                result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part_serial_overlapped": sim,
-                                                 "max_serial": max(x[0] for x in sim),
-                                                 "max_overlapped": max(x[1] for x in sim)}
-            else:
-                result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
-                                                 "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
+            result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
+                                             "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
 
-    # ---- CPU baseline: the oracle (C, OpenMP) on every k-th column of the same frame -----------
+    # ---- CPU baseline: the oracle's sources at -O3 (C, OpenMP) on a column sample of the frame -----
     if rank == 0 and world == 1 and host_vol is not None:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        S = O.OracleSession()
-        oh = S.new()
-        ovol = O.OVolume(host_vol.reshape((n, n, n), order="F"), 10)
-        S.sync_volumes(oh, 0, ovol, O.OVolume(refl.Data, 5), ovol)
-        L6 = np.array([list(l.Position) + list(l.Color) for l in lights], np.float32)
-        cols = np.arange(0, W, args.cpu_stride, dtype=np.int64)
-        t1 = time.perf_counter()
-        img, cpu_samples = S.render(oh, L6, O.OVolume(lut.Data, 7), [1.0, 0.4, 0.6], [1, 1, 1], [H, W],
-                                    np.flip(R, 0).astype(np.float32), [0, 3.0, 6.0], 0.9, [1, 1, 0],
-                                    threads=threads, cols=cols)
-        cpu_s = time.perf_counter() - t1
-        gpu_img = full if full is not None and world > 1 else out_local
-        g = gpu_img[: 3 * W * H].view(3, W, H).cpu().numpy()
-        o = np.transpose(img, (2, 1, 0))  # [H,W,3] F-order -> (3, W, H) C-order view
-        d = np.abs(g[:, cols, :] - o[:, cols, :])
-        result["cpu_baseline"] = {
-            "value": round(len(cols) * H / cpu_s / 1e6, 5), "unit": "Mrays/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle/vr_oracle.c (scalar C restatement, OpenMP) on every {args.cpu_stride}th column "
-                      f"({len(cols)} cols x {H} rays, {cpu_samples} samples) of the same frame, {cpu_s:.1f} s"}
-        result["parity_sampled_columns"] = {
-            "max_abs": float(d.max()), "img_max": float(np.abs(o[:, cols, :]).max()),
-            "bit_exact_frac": float((g[:, cols, :].view(np.uint32) == o[:, cols, :].view(np.uint32)).mean())}
+        result["cpu_baseline"], result["parity_sampled_columns"] = cpu_baseline(
+            args, host_vol, n, W, H, refl, lut, lights, R, full if world > 1 else out_local)
 
     if rank == 0:
-        # roofline.traffic: HBM bytes per launch from the rocprofv3 PMC passes committed under
-        # profiles/ (FETCH_SIZE + WRITE_SIZE with the gfx950 x2 FETCH_SIZE correction, calibrated
-        # on the stats kernel's known 4.3 GB read); only when it was measured on this workload.
+        # roofline.traffic / .valu: per-launch HBM bytes and VALU instructions of the march kernel
+        # from the rocprofv3 PMC passes committed under profiles/ (tools/profile_summary.py;
+        # FETCH_SIZE x 2 KiB + WRITE_SIZE KiB, the x2 being the gfx950 64-B-per-128-B-request tally);
+        # only when they were measured on this workload.
         try:
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
             if world == 1 and tj.get("workload") == result["config"]["workload"]:
+                src = os.path.relpath(args.traffic_json, ROOT)
                 result["roofline"]["traffic"] = tj["bytes_per_launch"]
-                result["roofline"]["traffic_source"] = os.path.relpath(args.traffic_json, ROOT) + \
-                    " (" + tj.get("method", "") + ")"
+                result["roofline"]["traffic_source"] = src + " (" + tj.get("method", "") + ")"
+                vi = tj.get("valu_insts_per_launch")
+                if vi:
+                    peak = VALU_ISSUE_PER_S
+                    result["roofline"]["valu"] = {
+                        "insts_per_launch": vi, "achieved": round(vi / t_kernel_s / 1e9, 2),
+                        "peak": round(peak / 1e9, 1), "unit": "G wave64-instr/s",
+                        "frac": round(vi / t_kernel_s / peak, 4),
+                        "source": src + " (SQ_INSTS_VALU; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 "
+                                        "VALU instruction, MI355X_MICROARCH.md)"}
         except (OSError, ValueError, KeyError):
             pass
         print(json.dumps(result), flush=True)
     vr.volumeRender("delete", h)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_share():
+    """CPUs this process may use: its affinity mask, capped by a cgroup-v2 CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline_lib():
+    """The CPU baseline's library: the oracle's sources rebuilt here with -O3 -march=native when gcc
+    is present (a few seconds), else the prebuilt -O3 -march=x86-64-v3 oracle/libcpubase.so."""
+    import subprocess
+    import tempfile
+    od = os.path.join(ROOT, "oracle")
+    out = os.path.join(tempfile.mkdtemp(prefix="vr_cpubase_"), "libcpubase_native.so")
+    flags = ["-O3", "-march=native", "-fPIC", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fopenmp"]
+    try:
+        subprocess.run(["gcc", *flags, "-shared", "-o", out, os.path.join(od, "vr_oracle.c"),
+                        os.path.join(od, "vr_oracle_host.c"), "-lm"], check=True, capture_output=True, timeout=120)
+        return out, "gcc " + " ".join(flags)
+    except (OSError, subprocess.SubprocessError):
+        return os.path.join(od, "libcpubase.so"), "prebuilt oracle/libcpubase.so (-O3 -march=x86-64-v3)"
+
+
+def cpu_baseline(args, host_vol, n, W, H, refl, lut, lights, R, gpu_out):
+    """The oracle's scalar C restatement at -O3, OpenMP over columns, on every CPU this process may
+    use and on one core, each on a column sample of the same frame; plus the sampled-column diff
+    of the GPU image against it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    path, build = cpu_baseline_lib()
+    share = cpu_share()
+    threads = args.cpu_threads or share
+    S = O.OracleSession()
+    oh = S.new()
+    ovol = O.OVolume(host_vol.reshape((n, n, n), order="F"), 10)
+    S.sync_volumes(oh, 0, ovol, O.OVolume(refl.Data, 5), ovol)
+    L6 = np.array([list(l.Position) + list(l.Color) for l in lights], np.float32)
+    rargs = (L6, O.OVolume(lut.Data, 7), [1.0, 0.4, 0.6], [1, 1, 1], [H, W], np.flip(R, 0).astype(np.float32),
+             [0, 3.0, 6.0], 0.9, [1, 1, 0])
+
+    def run(stride, nthreads):
+        cols = np.arange(0, W, stride, dtype=np.int64)
+        t1 = time.perf_counter()
+        img, samples = S.render(oh, *rargs, threads=nthreads, cols=cols, lib_path=path)
+        return cols, img, samples, time.perf_counter() - t1
+
+    cols, img, cpu_samples, cpu_s = run(args.cpu_stride, threads)
+    cols1, _, samples1, cpu1_s = run(args.cpu_stride_1core, 1)
+    g = gpu_out[: 3 * W * H].view(3, W, H).cpu().numpy()
+    o = np.transpose(img, (2, 1, 0))  # [H,W,3] F-order -> (3, W, H) C-order view
+    d = np.abs(g[:, cols, :] - o[:, cols, :])
+    base = {
+        "value": round(len(cols) * H / cpu_s / 1e6, 5), "unit": "Mrays/s", "cores": threads,
+        "kind": "port",
+        "sample": f"oracle/vr_oracle.c (scalar C restatement, OpenMP over columns; {build}) on every "
+                  f"{args.cpu_stride}th column ({len(cols)} cols x {H} rays, {cpu_samples} samples) of the same "
+                  f"frame, {cpu_s:.1f} s on {threads} threads",
+        "host_cpus": os.cpu_count(), "cpu_share": share,
+        "one_core": {"value": round(len(cols1) * H / cpu1_s / 1e6, 6), "unit": "Mrays/s", "cores": 1,
+                     "sample": f"every {args.cpu_stride_1core}th column ({len(cols1)} cols x {H} rays, "
+                               f"{samples1} samples), {cpu1_s:.1f} s"}}
+    parity = {"max_abs": float(d.max()), "img_max": float(np.abs(o[:, cols, :]).max()),
+              "bit_exact_frac": float((g[:, cols, :].view(np.uint32) == o[:, cols, :].view(np.uint32)).mean())}
+    return base, parity
+
+
+def _latest_traffic_json():
+    """profiles/<latest round>/traffic.json (the newest PMC pass committed)."""
+    import glob
+    c = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*", "traffic.json")),
+               key=lambda p: int("".join(ch for ch in os.path.basename(os.path.dirname(p)) if ch.isdigit()) or 0))
+    return c[-1] if c else os.path.join(ROOT, "profiles", "round1", "traffic.json")
 
 
 if __name__ == "__main__":

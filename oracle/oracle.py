@@ -44,16 +44,19 @@ class OrParams(ctypes.Structure):
                 ("gx", OrTex), ("gy", OrTex), ("gz", OrTex), ("lut", OrTex)]
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(path: str = LIB_PATH):
+    """The oracle's shared object (default liboracle.so).  bench.py's cpu_baseline leg passes the
+    -O3 build of the same sources (libcpubase.so, or a -march=native build made on the box)."""
+    if path not in _libs:
+        if not os.path.exists(path):
             raise ImportError(f"oracle not built: make -C {_HERE}")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         for sfx in ("f32", "f64"):
+            if not hasattr(L, f"or_render_{sfx}"):  # libcpubase.so: f32 only
+                continue
             f = getattr(L, f"or_render_{sfx}")
             f.restype = c_uint64
             f.argtypes = [POINTER(OrParams), c_void_p, c_void_p, c_int64, c_int]
@@ -69,8 +72,8 @@ def lib():
         L.or_grad_step.argtypes = [c_uint64, c_uint64, c_uint64, c_void_p]
         L.or_hg_lut.restype = c_int
         L.or_hg_lut.argtypes = [c_uint, c_float, c_void_p]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def hg_lut(n: int, g: float = 0.8) -> np.ndarray:
@@ -302,13 +305,15 @@ class OracleSession:
         degenerate = not finite
         return P, keep, degenerate
 
-    def render(self, h: int, *args, double: bool = False, threads: int = 0, cols=None, pixels=None, **kw):
+    def render(self, h: int, *args, double: bool = False, threads: int = 0, cols=None, pixels=None,
+               lib_path: str = LIB_PATH, **kw):
         """Returns (image [H,W,3] float32 column-major, total samples).  With `pixels=(xs, ys)`
         returns (values [n,3], per-pixel samples) instead."""
         P, keep, degenerate = self.params(h, *args, **kw)
         threads = threads or os.cpu_count() or 1
-        f = lib().or_render_f64 if double else lib().or_render_f32
-        fp = lib().or_render_pixels_f64 if double else lib().or_render_pixels_f32
+        L = lib(lib_path)
+        f = L.or_render_f64 if double else L.or_render_f32
+        fp = L.or_render_pixels_f64 if double else L.or_render_pixels_f32
         if pixels is not None:
             xs = np.ascontiguousarray(pixels[0], dtype=np.int64)
             ys = np.ascontiguousarray(pixels[1], dtype=np.int64)

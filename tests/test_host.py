@@ -211,13 +211,21 @@ def test_no_silent_cpu_fallback_without_gpu():
 
 
 def test_committed_traffic_matches_bench_default_workload():
-    """bench.py reports roofline.traffic only when profiles/round1/traffic.json was measured on its
-    default workload (the metric config); the key must match verbatim."""
+    """bench.py reports roofline.traffic / .valu only when the newest profiles/<round>/traffic.json
+    was measured on its default workload (the metric config); the key must match verbatim."""
     import json
     import sys
     sys.path.insert(0, ROOT)
     import bench
-    with open(os.path.join(ROOT, "profiles", "round1", "traffic.json")) as fh:
+    path = bench._latest_traffic_json()
+    with open(path) as fh:
         tj = json.load(fh)
     assert tj["workload"] == bench.workload_name(1024, 1920, 1080, 2, "compute")
     assert tj["bytes_per_launch"] > 0
+
+
+def test_cpu_share_is_positive():
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    assert 1 <= bench.cpu_share() <= (os.cpu_count() or 1)

@@ -54,9 +54,14 @@ march = r"march_kernel<\d, 1, true, false, false, false, \d+, false>"
 fetch_kb, write_kb = mean(march, "FETCH_SIZE"), mean(march, "WRITE_SIZE")
 if fetch_kb is not None:
     traffic = 2 * 1024 * fetch_kb + 1024 * (write_kb or 0.0)
+    extra = {c: mean(march, c) for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU",
+                                          "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_ACTIVE_INST_VALU",
+                                          "TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum", "GRBM_GUI_ACTIVE")}
     with open(os.path.join(out, "traffic.json"), "w") as fh:
         json.dump({"workload": workload, "kernel": march, "fetch_size_kib": fetch_kb, "write_size_kib": write_kb,
                    "bytes_per_launch": traffic,
+                   "valu_insts_per_launch": extra["SQ_INSTS_VALU"],
+                   "counters_per_launch": {k: v for k, v in extra.items() if v is not None},
                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; read bytes = 2 x 1024 x FETCH_SIZE "
                              "(gfx950 64 B tally per 128 B request)"}, fh, indent=1)
     print("traffic bytes/launch", traffic)
