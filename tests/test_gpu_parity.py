@@ -337,20 +337,22 @@ def test_step_count_matches_oracle(counter_clock):
     r.delete()
 
 
+@pytest.mark.parametrize("edge", [56, 64])
 @pytest.mark.parametrize("shade", ["fast", "exact"])
 @pytest.mark.parametrize("scene", ["hg2", "lookup", "ea"])
-def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, shade):
+def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, shade, edge):
     """The LDS-staged march, the plain kernel, the empty-sample skip / empty-chunk leap and the
     XCD tile order, the longest-first workgroup schedule (every repeated frame shape after the first
     launch) and the depth lanes (K lanes per ray compositing K consecutive samples) change
     only where data comes from, which exact no-ops are elided and which lane computes a sample:
     the images must agree bit for bit, with either shading arithmetic.  The image
-    size is ragged for every tile shape."""
+    size is ragged for every tile shape.  Edge 64 (a power-of-two cube) takes the fast variant's
+    half-texel gradient taps in every kernel."""
     if shade == "exact":
         monkeypatch.setenv("VR_EXACT_SHADE", "1")
     else:
         monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
-    v = vr.Volume(O.shell_volume(56))
+    v = vr.Volume(O.shell_volume(edge))
     r = ex1_renderer(v, res=(121, 87), lights=(scene != "ea"))
     if scene == "lookup":
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
@@ -376,6 +378,29 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
     assert base.max() > 0
     for name, img in imgs.items():
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
+    r.delete()
+
+
+@pytest.mark.parametrize("edge", [64, 128])
+def test_half_texel_taps(monkeypatch, counter_clock, edge):
+    """Fast variant on a power-of-two cube (vr_capi.hip half_texel_taps): the on-the-fly gradient
+    taps derived from the centre's axes equal the reference's pos +- gstep taps except near the
+    planes where a coordinate changes binade.  Both renders are within the oracle tolerance, and
+    they differ in at most a few pixel-channels, by little."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(edge))
+    r = ex1_renderer(v, res=(160, 128))
+    monkeypatch.setenv("VR_EXACT_TAPS", "1")
+    exact = r.render()
+    monkeypatch.delenv("VR_EXACT_TAPS")
+    fast = r.render()
+    assert len(tee.renders) == 2
+    differ = float((fast.view(np.uint32) != exact.view(np.uint32)).mean())
+    print("half-texel taps: pixel-channels differing", differ, "max", float(np.abs(fast - exact).max()),
+          "of", float(exact.max()))
+    assert differ < 2e-3
+    assert np.abs(fast - exact).max() <= 1e-3 * exact.max()
     r.delete()
 
 

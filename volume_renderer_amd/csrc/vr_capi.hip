@@ -457,6 +457,26 @@ bool same_dims(const vr::DevTex &a, const vr::DevTex &b) {
 // finite and comfortably below FLT_MAX (a texture that is unbound reads 0)
 bool tame(const BufPtr &b) { return !b || !b->ptr || (!b->nonfinite && b->maxabs < 1e30f); }
 
+// Whether the fast variant may derive the on-the-fly gradient taps from the centre's axes
+// (vr_sampling.h half_taps): a cube of power-of-two edge n with isotropic element
+// size, i.e. on every axis box [-1, 1] (bscale 1/2), gstep = 1/n exact and a tap offset of exactly
+// half a texel.  Then the reference's tap coordinate ((pos + 2^-k) + 1) * 1/2 * n - 1/2 equals the
+// centre's xb +- 1/2 exactly -- adding 2^-k (a multiple of the ulp of pos + 1 in [1, 2)) commutes with
+// the rounding of pos + 1 -- except for samples within half a texel of a plane where pos, pos +- 2^-k
+// or pos + 1 changes binade (pos = 0, +-2^-j), where the two can differ by an ulp of pos before the
+// 8-bit weight quantization (measured: tests/test_gpu_parity.py::test_half_texel_taps).
+// VR_EXACT_TAPS=1 turns it off.
+int32_t half_texel_taps(const vr::RenderParams &P, int mode, float fnz) {
+  if (mode != 1 || env_flag("VR_EXACT_TAPS")) return 0;
+  const float n[3] = {P.em.fnx, P.em.fny, fnz};
+  for (int i = 0; i < 3; ++i) {
+    int e = 0;
+    if (!(n[i] >= 2.f) || std::frexp(n[i], &e) != 0.5f) return 0;  // power of two
+    if (P.gstep[i] != 1.f / n[i] || P.bscale[i] != 0.5f || P.bmin[i] != -1.f) return 0;
+  }
+  return 1;
+}
+
 // initRender (volumeRender.cpp:112-156) + the per-frame constants of d_render.
 struct Frame {
   vr::RenderParams P;
@@ -549,6 +569,7 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
       F.drift1[i] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[i] * (double)n;
       P.tap_off[i] = (float)((F.mode == 1 ? (double)P.gstep[i] * P.bscale[i] * n : 0.0) + 0.0625);
     }
+    P.tap_half = half_texel_taps(P, F.mode, P.em.fnz);
   }
   // Empty-sample skip: a sample with alpha == 0 adds fma(eds, c, ill) * 0 to the
   // sum; that is exactly +-0 (a no-op) whenever the illumination term `ill` is finite, which holds
@@ -897,6 +918,7 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
     for (int i = 0; i < 3; ++i) pmax = std::max(pmax, (double)std::fabs(P.bmin[i]) + std::fabs(P.eye[i]));
     F.drift1[2] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[2] * D;
     P.tap_off[2] = (float)((F.mode == 1 ? (double)P.gstep[2] * P.bscale[2] * D : 0.0) + 0.0625);
+    P.tap_half = half_texel_taps(P, F.mode, (float)D);  // judged on the whole volume, as one render
   }
   set_chunk_halo(F, 4);  // the slab launch marches with up to 4 depth lanes (chunks <= 64 samples)
   P.slab_margin = P.tap_off[2] / P.em.fnz;  // bound of the chunk ownership test, normalized

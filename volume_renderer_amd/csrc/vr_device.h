@@ -51,6 +51,8 @@ struct RenderParams {
   float color[3];
   float gstep[3];                 // gradient step (world units)          volumeRender.cpp:273-275
   float tap_off[3];               // gradient tap offset in emission texels (staging halo)
+  int32_t tap_half;               // MODE 1: the tap offset is half a texel on every axis (fast
+                                  // variant derives the taps from the centre, vr_sampling.h)
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;

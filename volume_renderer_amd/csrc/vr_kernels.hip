@@ -93,7 +93,16 @@ __global__ __launch_bounds__(256, VR_MIN_WAVES) void render_kernel(const RenderP
             const float ym = ((pos.y - P.gstep[1]) - bmin.y) * bsc.y;
             const float zp = ((pos.z + P.gstep[2]) - bmin.z) * bsc.z;
             const float zm = ((pos.z - P.gstep[2]) - bmin.z) * bsc.z;
-            if (SHARE) {  // gem == em: reuse the centre's axes on the unshifted coordinates
+            if (SHARE && FAST && P.tap_half) {  // half-texel taps derived from the centre (vr_march.hip)
+              const DevTex &T = P.gem;
+              Ax p, m;
+              half_taps(axis_raw_s(ps.x, T.fnx), p, m);
+              g.x = fetch<BIG>(T, clamp_ax(p, T.nx), ay, az) - fetch<BIG>(T, clamp_ax(m, T.nx), ay, az);
+              half_taps(axis_raw_s(ps.y, T.fny), p, m);
+              g.y = fetch<BIG>(T, ax, clamp_ax(p, T.ny), az) - fetch<BIG>(T, ax, clamp_ax(m, T.ny), az);
+              half_taps(axis_raw_s(ps.z, T.fnz), p, m);
+              g.z = fetch<BIG>(T, ax, ay, clamp_ax(p, T.nz)) - fetch<BIG>(T, ax, ay, clamp_ax(m, T.nz));
+            } else if (SHARE) {  // gem == em: reuse the centre's axes on the unshifted coordinates
               const DevTex &T = P.gem;
               g.x = fetch<BIG>(T, axis(xp, T.nx, T.fnx), ay, az) - fetch<BIG>(T, axis(xm, T.nx, T.fnx), ay, az);
               g.y = fetch<BIG>(T, ax, axis(yp, T.ny, T.fny), az) - fetch<BIG>(T, ax, axis(ym, T.ny, T.fny), az);

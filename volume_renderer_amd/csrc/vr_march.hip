@@ -102,9 +102,23 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
   const float tstep = P.tstep;
   const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
-  // unclamped axes (axis_raw): exact on the LDS path, clamped by fetch_at on the global one
-  const Ax ax = axis_raw<NANCHK>(ps.x, E.fnx), ay = axis_raw<NANCHK>(ps.y, E.fny),
-           az = axis_raw<NANCHK>(ps.z, E.fnz);
+  // unclamped axes (axis_raw): exact on the LDS path, clamped by fetch_at on the global one.
+  // The fast variant's half-texel gradient taps need the raw fraction's half split as well.
+  constexpr bool HALF_TAPS = VR_MARCH_FAST && MODE == 1;
+  AxS sx{}, sy{}, sz{};
+  Ax ax, ay, az;
+  if constexpr (HALF_TAPS) {
+    sx = axis_raw_s<NANCHK>(ps.x, E.fnx);
+    sy = axis_raw_s<NANCHK>(ps.y, E.fny);
+    sz = axis_raw_s<NANCHK>(ps.z, E.fnz);
+    ax = Ax{sx.i, sx.w};
+    ay = Ax{sy.i, sy.w};
+    az = Ax{sz.i, sz.w};
+  } else {
+    ax = axis_raw<NANCHK>(ps.x, E.fnx);
+    ay = axis_raw<NANCHK>(ps.y, E.fny);
+    az = axis_raw<NANCHK>(ps.z, E.fnz);
+  }
   // centre cell in the slot; the gradient taps below differ from it along one axis only
   const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
   const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
@@ -123,6 +137,27 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     f3 g;
     if (MODE == 1 && (VR_ABLATE & 4)) {
       g = mk(ps.x, ps.y, em_s);
+    } else if (HALF_TAPS && P.tap_half) {
+      // fast variant, gradient offset of exactly half a texel on every axis (a cube volume with
+      // isotropic element size): each axis' two taps derived from the centre's (half_taps), the
+      // minus tap's cell one slot word below the plus tap's
+      const bool syz = staged && iny && inz, sxz = staged && inx && inz, sxy = staged && inx && iny;
+      Ax p, m;
+      half_taps(sx, p, m);
+      int lp = slot_coord(p.i, B.rx);
+      g.x = fetch_at<BIG>(E, L, B, syz && in_box(lp, B.ex), ayz + lp, p, ay, az) -
+            fetch_at<BIG>(E, L, B, syz && in_box(lp - 1, B.ex), ayz + lp - 1, m, ay, az);
+      half_taps(sy, p, m);
+      lp = slot_coord(p.i, B.ry);
+      const int axz = lz * B.pxy + lx;
+      g.y = fetch_at<BIG>(E, L, B, sxz && in_box(lp, B.ey), axz + lp * B.px, ax, p, az) -
+            fetch_at<BIG>(E, L, B, sxz && in_box(lp - 1, B.ey), axz + (lp - 1) * B.px, ax, m, az);
+      half_taps(sz, p, m);
+      lp = slot_coord(p.i, B.rz);
+      const int axy = ly * B.px + lx;
+      g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lp, B.ez), axy + lp * B.pxy, ax, ay, p) -
+            fetch_at<BIG>(E, L, B, sxy && in_box(lp - 1, B.ez), axy + (lp - 1) * B.pxy, ax, ay, m);
+      g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
     } else if (MODE == 1) {  // computeGradient on tex_emission (gem == em), world offsets +-gstep
       const float xp = ((pos.x + P.gstep[0]) - bmin.x) * bsc.x;
       const float xm = ((pos.x - P.gstep[0]) - bmin.x) * bsc.x;

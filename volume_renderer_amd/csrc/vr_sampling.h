@@ -52,6 +52,36 @@ __device__ __forceinline__ Ax axis_raw(float c, float fn) {
 }
 __device__ __forceinline__ Ax clamp_ax(const Ax &a, int n) { return Ax{min(max(a.i, -1), n - 1), a.w}; }
 
+// axis_raw plus the half-texel split of the raw fraction (frac(xb) >= 0.5), for the fast
+// gradient taps of a half-texel tap offset (half_taps below).
+struct AxS {
+  int i;
+  float w;
+  bool hi;
+};
+template <bool NANCHK = true>
+__device__ __forceinline__ AxS axis_raw_s(float c, float fn) {
+  if (NANCHK) c = (c != c) ? 0.f : c;  // NaN coordinate -> 0 (every tap of it is then the centre's
+                                       // clamped edge voxel: g = 0, as the reference's NaN taps)
+  const float xb = c * fn - 0.5f;
+  const float fl = floorf(xb);
+  const float r = xb - fl;
+  const float w = rintf(r * 256.f) * (1.f / 256.f);
+  return AxS{(int)fl, w, r >= 0.5f};
+}
+// The two taps xb +- 1/2 of an axis derived from the centre's (fast shading variant, DESIGN.md
+// s4): with xb' = xb + 1/2 computed exactly, floor(xb') = i + hi and the quantized weight of
+// frac(xb') is w + 1/2 - hi (rint((r + 1/2 - hi) * 256) = rint(r * 256) + 128 - 256 hi: adding an
+// even integer keeps round-half-even); xb - 1/2 has the same weight on the cell one lower.  The
+// reference forms each tap coordinate from pos +- gstep in fp32, which can differ from xb +- 1/2
+// in its last bits; the difference reaches an 8-bit weight or a cell only at rounding boundaries.
+__device__ __forceinline__ void half_taps(const AxS &a, Ax &plus, Ax &minus) {
+  const int ip = a.i + (a.hi ? 1 : 0);
+  const float wt = a.w + (a.hi ? -0.5f : 0.5f);
+  plus = Ax{ip, wt};
+  minus = Ax{ip - 1, wt};
+}
+
 // Correctly rounded sqrtf for x >= 0, NaN or +inf.  The device library's sqrtf scales inputs
 // below 2^-96 and patches +-0 / inf by class; for x == 0 or x >= 2^-96 its remaining steps (the
 // hardware root corrected by one ulp either way from two fma residuals) give the identical result
