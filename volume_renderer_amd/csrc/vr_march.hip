@@ -63,12 +63,12 @@ template <int K, int I>
 __device__ __forceinline__ float group_lane(float v) {
   if constexpr (K == 1) {
     return v;
-  } else if constexpr (K == 2) {
+  } else if constexpr (K == 2) {  // quad_perm reads lanes of the same quad: no old value needed
     constexpr int ctrl = I | (I << 2) | ((2 + I) << 4) | ((2 + I) << 6);
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xf, 0xf, true));
   } else if constexpr (K == 4) {
     constexpr int ctrl = I | (I << 2) | (I << 4) | (I << 6);
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xf, 0xf, true));
   } else {
     static_assert(K == 8, "depth lanes: K in {1, 2, 4, 8}");
     return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (I << 5)));
@@ -138,25 +138,27 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     if (MODE == 1 && (VR_ABLATE & 4)) {
       g = mk(ps.x, ps.y, em_s);
     } else if (HALF_TAPS && P.tap_half) {
-      // fast variant, gradient offset of exactly half a texel on every axis (a cube volume with
-      // isotropic element size): each axis' two taps derived from the centre's (half_taps), the
-      // minus tap's cell one slot word below the plus tap's
+      // fast variant, gradient offset of exactly half a texel on every axis (a power-of-two cube,
+      // vr_capi.hip half_texel_taps): each axis' two taps derived from the centre's (half_taps);
+      // in the slot the plus tap's cell is the centre's, or the next one along the axis, and the
+      // minus tap's lies one row / plane below it
       const bool syz = staged && iny && inz, sxz = staged && inx && inz, sxy = staged && inx && iny;
       Ax p, m;
       half_taps(sx, p, m);
-      int lp = slot_coord(p.i, B.rx);
-      g.x = fetch_at<BIG>(E, L, B, syz && in_box(lp, B.ex), ayz + lp, p, ay, az) -
-            fetch_at<BIG>(E, L, B, syz && in_box(lp - 1, B.ex), ayz + lp - 1, m, ay, az);
+      int l = lx + (sx.hi ? 1 : 0);
+      int a = ac + (sx.hi ? 1 : 0);
+      g.x = fetch_at<BIG>(E, L, B, syz && in_box(l, B.ex), a, p, ay, az) -
+            fetch_at<BIG>(E, L, B, syz && in_box(l - 1, B.ex), a - 1, m, ay, az);
       half_taps(sy, p, m);
-      lp = slot_coord(p.i, B.ry);
-      const int axz = lz * B.pxy + lx;
-      g.y = fetch_at<BIG>(E, L, B, sxz && in_box(lp, B.ey), axz + lp * B.px, ax, p, az) -
-            fetch_at<BIG>(E, L, B, sxz && in_box(lp - 1, B.ey), axz + (lp - 1) * B.px, ax, m, az);
+      l = ly + (sy.hi ? 1 : 0);
+      a = ac + (sy.hi ? B.px : 0);
+      g.y = fetch_at<BIG>(E, L, B, sxz && in_box(l, B.ey), a, ax, p, az) -
+            fetch_at<BIG>(E, L, B, sxz && in_box(l - 1, B.ey), a - B.px, ax, m, az);
       half_taps(sz, p, m);
-      lp = slot_coord(p.i, B.rz);
-      const int axy = ly * B.px + lx;
-      g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lp, B.ez), axy + lp * B.pxy, ax, ay, p) -
-            fetch_at<BIG>(E, L, B, sxy && in_box(lp - 1, B.ez), axy + (lp - 1) * B.pxy, ax, ay, m);
+      l = lz + (sz.hi ? 1 : 0);
+      a = ac + (sz.hi ? B.pxy : 0);
+      g.z = fetch_at<BIG>(E, L, B, sxy && in_box(l, B.ez), a, ax, ay, p) -
+            fetch_at<BIG>(E, L, B, sxy && in_box(l - 1, B.ez), a - B.pxy, ax, ay, m);
       g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
     } else if (MODE == 1) {  // computeGradient on tex_emission (gem == em), world offsets +-gstep
       const float xp = ((pos.x + P.gstep[0]) - bmin.x) * bsc.x;
@@ -226,15 +228,17 @@ __device__ __forceinline__ bool group_any(bool b) {
   return ((m >> base) & ((1ull << K) - 1)) != 0ull;
 }
 
-// Composite the existing samples (a prefix of nv of the K) of a depth-lane group in order, every
-// lane of the group alike; the ray stops at the first sum.a > thr (volumeRender_kernel.cu:482).
+// Composite the existing samples (a prefix of the K; exf = 1 where this lane's sample exists) of a
+// depth-lane group in order, every lane of the group alike; the ray stops at the first sum.a > thr
+// (volumeRender_kernel.cu:482).
 template <int K, int I>
-__device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, int nv, float r, float gg, float b,
+__device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, float exf, float r, float gg, float b,
                                                 float alpha) {
   if constexpr (I < K) {
     const float ri = group_lane<K, I>(r), gi = group_lane<K, I>(gg), bi = group_lane<K, I>(b),
                 ai = group_lane<K, I>(alpha);
-    if (I < nv && R.alive) {
+    // sample I of the group exists iff group lane I's does (the existing samples are a prefix)
+    if (group_lane<K, I>(exf) != 0.f && R.alive) {
       const float om = 1.f - R.sa;
       R.sr = fmaf(om, ri, R.sr);
       R.sg = fmaf(om, gi, R.sg);
@@ -242,7 +246,7 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, i
       R.sa = fmaf(om, ai, R.sa);
       if (R.sa > P.thr) R.alive = false;
     }
-    composite_group<K, I + 1>(P, R, nv, r, gg, b, alpha);
+    composite_group<K, I + 1>(P, R, exf, r, gg, b, alpha);
   }
 }
 
@@ -401,9 +405,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           bool shaded;
           sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
         }
-        const uint64_t m = __ballot(ex);
-        const int nv = __popcll((m >> (lane & ~(K - 1))) & ((1ull << K) - 1));  // existing samples
-        composite_group<K, 0>(P, R, nv, r, gg, b, alpha);
+        composite_group<K, 0>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
         if constexpr (SLAB) {
           if (R.alive && group_any<K>(R.mine && !ex)) {  // left the slab still unfinished
             R.alive = false;

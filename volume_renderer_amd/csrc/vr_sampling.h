@@ -144,18 +144,23 @@ __device__ __forceinline__ float fetch(const DevTex &t, const Ax &ax, const Ax &
   return lerp(c0, c1, az.w);
 }
 
-// Axis of a texture whose offsets are formed in fp32 (fetch_small): the clamped floor kept as a
-// float (the same value axis() converts) and the weight.
+// Axis of a texture whose offsets are formed in fp32 (fetch_small): the floor kept as a float
+// (the value axis() would convert) and the weight.
 struct AxF {
   float fl;
   float w;
 };
-__device__ __forceinline__ AxF axis_f(float c, float fn) {
-  c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
+
+// axis_f for a LUT coordinate, an angle / pi: in [0, 1] or NaN (acosf / acospi of a quotient
+// that is NaN or rounds past +-1).  One v_med3 does the NaN -> 0 substitution (the median of NaN,
+// 0 and 1 is min3 = 0 under the hardware's NaN rule) and keeps c in [0, 1], where the floor of
+// c*n - 0.5 is already in [-1, n-1]: the same axis as axis_f, without its compare, select and clamp.
+__device__ __forceinline__ AxF axis_lut(float c, float fn) {
+  c = __builtin_amdgcn_fmed3f(c, 0.f, 1.f);
   const float xb = c * fn - 0.5f;
   const float fl = floorf(xb);
   const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
-  return AxF{__builtin_amdgcn_fmed3f(fl, -1.f, fn - 1.f), w};
+  return AxF{fl, w};
 }
 
 // Trilinear fetch from a texture of fewer than 2^22 padded voxels (the illumination LUT): the
@@ -184,7 +189,7 @@ __device__ __forceinline__ float lut_light(const DevTex &lut, const AxF &la, flo
     const float q = lut.p[0];
     return fmaf(0.5f, q - q, q);
   }
-  const AxF lb = axis_f(beta, lut.fny), lg = axis_f(gamma, lut.fnz);
+  const AxF lb = axis_lut(beta, lut.fny), lg = axis_lut(gamma, lut.fnz);
   if (lut.small) return fetch_small(lut, la, lb, lg);
   return fetch<false>(lut, to_ax(la), to_ax(lb), to_ax(lg));
 }
@@ -375,7 +380,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
     const float rn = __builtin_amdgcn_rsqf(dot3(n, n)), rlip = __builtin_amdgcn_rsqf(dot3(lip, lip));
     const float alpha_n = acospi_q(dot3(n, li) * (rn * __builtin_amdgcn_rsqf(dot3(li, li))));
-    const AxF la = axis_f(alpha_n, P.lut.fnx);
+    const AxF la = axis_lut(alpha_n, P.lut.fnx);
     int i = 0;
     for (; i + 1 < P.num_lights; i += 2) {
       const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
@@ -436,7 +441,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       alpha_n = divpi(acosf(q[0]));
 #endif
     }
-    const AxF la = axis_f(alpha_n, P.lut.fnx);
+    const AxF la = axis_lut(alpha_n, P.lut.fnx);
     // lights two at a time: both angle pairs, then both LUT fetches (their loads overlap), then the
     // accumulation in light order, exactly as the reference's sequential loop
     int i = 0;
