@@ -97,8 +97,14 @@ int vr_delete(vr_context *h);
 int vr_mem_info(vr_context *h, char *buf, size_t buflen);
 
 /* 'sync_volumes' (render.cpp:93-129): note the order Emission, Reflection, Absorption.
- * dx, dy, dz all non-NULL: the 9-argument form (gradient lookup); all NULL: the 6-argument form
- * (gradient volumes reset, on-the-fly gradient). */
+ * The reference keys on the argument count (render.cpp:105-113), mapped to the gradient pointers:
+ *   dx, dy, dz all non-NULL  -- nrhs == 9: the gradient volumes are taken (gradient lookup);
+ *   all NULL                 -- nrhs == 6: the handle's gradient volumes are reset (on-the-fly);
+ *   dx (nrhs 7) or dx, dy (nrhs 8) non-NULL, the rest NULL -- any other count (an adaptor passes
+ *                              nrhs 7, 8 or > 9 this way): the handle KEEPS its previous gradient
+ *                              volumes and the given ones are not read; the method is set to
+ *                              on-the-fly, and the sync re-enters lookup mode if kept gradient
+ *                              volumes exist (mmanager.hxx:193-200). */
 int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume *emission,
                     const vr_volume *reflection, const vr_volume *absorption, const vr_volume *dx,
                     const vr_volume *dy, const vr_volume *dz);

@@ -2,7 +2,8 @@
 // `volumeRender` that keeps the reference's command protocol (src/C/mex/render.cpp:50-278) so that
 // VolumeRender.m / Volume.m / LightSource.m run unchanged on MI355X.
 //
-// Not built in this repository (it needs MATLAB's mex.h / libmx); a maintainer builds it with
+// Built here only against the test stand-in of MATLAB's API (tests/mexstub/: a test-only mex.h and
+// mxArray model, driven by tests/test_mex_adaptor.py); a maintainer builds the real MEX with
 //   mex -R2018a -I<repo>/include -L<repo>/volume_renderer_amd -lvrhip volumeRender_mex.cpp -output volumeRender
 // and puts the result where src/make.m put the CUDA mex (src/matlab/VolumeRender/).  See
 // INTEGRATION.md.  All marshalling permutations (reversed ElementSizeUm and light positions,
@@ -176,11 +177,14 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     if (nrhs < 6) mexErrMsgTxt("insufficient parameter!");
     const uint64_t t_sync = (uint64_t)mxGetScalar(prhs[2]);
     const vr_volume em = make_volume(prhs[3]), re = make_volume(prhs[4]), ab = make_volume(prhs[5]);
-    if (nrhs >= 9) {
+    if (nrhs == 9) {  // gradient volumes given (render.cpp:105-110)
       const vr_volume dx = make_volume(prhs[6]), dy = make_volume(prhs[7]), dz = make_volume(prhs[8]);
       check(vr_sync_volumes(h, t_sync, &em, &re, &ab, &dx, &dy, &dz));
-    } else {
+    } else if (nrhs == 6) {  // gradient volumes reset (render.cpp:111-112)
       check(vr_sync_volumes(h, t_sync, &em, &re, &ab, nullptr, nullptr, nullptr));
+    } else {  // 7, 8, > 9: the previous gradient volumes are kept; the extra arguments are not read
+      const vr_volume unread{};
+      check(vr_sync_volumes(h, t_sync, &em, &re, &ab, &unread, nrhs == 7 ? nullptr : &unread, nullptr));
     }
     if (nlhs != 0 || nrhs > 9) mexWarnMsgTxt("SyncVolumes: Unexpected arguments ignored.");
     return;

@@ -131,10 +131,11 @@ def _empty():
 
 
 class DevArray:
-    """A device copy ('cudaArray'): snapshot of the data at upload time."""
+    """A device copy ('cudaArray'): snapshot of the data at upload time.  copy=False keeps a view
+    (full-size tests whose volumes are never edited after the sync: no second 4-32 GiB copy)."""
 
-    def __init__(self, vol: OVolume):
-        self.data = np.array(np.asarray(vol.array, dtype=np.float32).reshape(-1, order="F"), copy=True)
+    def __init__(self, vol: OVolume, copy: bool = True):
+        self.data = np.array(np.asarray(vol.array, dtype=np.float32).reshape(-1, order="F"), copy=True if copy else None)
         self.dims = vol.dims
 
 
@@ -148,9 +149,10 @@ class Handle:
 class OracleSession:
     """The state the reference keeps across mex calls, and `render` on top of the C oracle."""
 
-    def __init__(self):
+    def __init__(self, copy: bool = True):
         self.handles = {}
         self._next = 1
+        self.copy = copy  # snapshot volumes at sync (False: views of the caller's arrays)
         self._reset_globals()
 
     def _reset_globals(self):
@@ -173,16 +175,20 @@ class OracleSession:
             o.arr = [None] * 7
 
     # 'sync_volumes'
-    def sync_volumes(self, h: int, t_sync: int, em, re, ab, gx=None, gy=None, gz=None) -> None:
+    def sync_volumes(self, h: int, t_sync: int, em, re, ab, gx=None, gy=None, gz=None, nrhs=None) -> None:
+        """render.cpp:93-129.  nrhs (the mex argument count, default 9 with gradients, else 6):
+        9 takes the gradient volumes, 6 resets them, any other count keeps the previous ones
+        (render.cpp:105-113); setGradientMethod(lookup if 9 else compute) precedes the sync."""
         m = self.handles[h]
         m.time_last_mem_sync = int(t_sync)
         m.vol[EM], m.vol[RE], m.vol[AB] = em, re, ab
-        lookup = gx is not None
-        if lookup:
+        if nrhs is None:
+            nrhs = 9 if gx is not None else 6
+        if nrhs == 9:
             m.vol[DX], m.vol[DY], m.vol[DZ] = gx, gy, gz
-        else:
+        elif nrhs == 6:
             self._reset_gradients(m)
-        self.grad_method = 1 if lookup else 0
+        self.grad_method = 1 if nrhs == 9 else 0
         self._mm_sync(m)
 
     def _reset_gradients(self, m):
@@ -191,7 +197,7 @@ class OracleSession:
 
     def _sync_volume(self, m, tex, slot):
         self.bind[tex] = None
-        m.arr[slot] = DevArray(m.vol[slot])
+        m.arr[slot] = DevArray(m.vol[slot], copy=self.copy)
         self.bind[tex] = m.arr[slot]
 
     def _reference(self, m, tex, bufslot, idxslot, target):

@@ -31,8 +31,9 @@ class Tee:
             self.S.delete(self.hmap.pop(int(args[0])))
         elif cmd == "sync_volumes":
             h = self.hmap[int(args[0])]
-            vols = [_ovol(v) for v in args[2:]]
-            self.S.sync_volumes(h, int(args[1]), *vols)
+            nrhs = 1 + len(args)
+            vols = [_ovol(v) for v in args[2:5]] + ([_ovol(v) for v in args[5:8]] if nrhs == 9 else [])
+            self.S.sync_volumes(h, int(args[1]), *vols, nrhs=nrhs)
         elif cmd in ("render", "render_stereo"):
             h = self.hmap[int(args[0])]
             lights, illum = args[1], args[2]

@@ -1,0 +1,366 @@
+"""Oracle parity at the FULL size of every BASELINE.json configuration, with the
+production kernels -- the launches a user's render takes (no sample counter, default depth lanes,
+the longest-first schedule of short launches) -- on a stratified pixel sample.
+
+The oracle (oracle/vr_oracle.c, fp32 + fp64 envelope) cannot march a whole 1920x1080 frame of a
+1024^3 volume inside a test, but it marches any chosen pixels exactly: each config is rendered whole
+on the GPU and ~9k of its pixels are checked against the oracle under the SURVEY.md 8c tolerance
+(envelope floored at its image RMS, conftest.assert_parity_full_size).
+The sample is stratified so that the hard rays are in it: uniform random pixels, the pixels with
+the longest chord through the box (most samples, most accumulated rounding) and the brightest
+pixels of the product image (most lit, shaded samples).  Volumes are generated in HBM
+(vr_synth_shell_device / torch) and copied back so that oracle and product read the same voxels.
+
+Configs (BASELINE.json "configs"):
+  C2      V_shell(1024), 1024x768, HG 2 lights (example1.m), on-the-fly gradient
+  metric  V_shell(1024), 1920x1080, same shading (the bench.py frame)
+  C3      V_shell(1024), 1920x1080, lookup gradient (4 volumes resident, interleaved copy)
+  C4      two channels (example3.m settings) x off-axis stereo, 1920x1080 per eye, + the 4-part
+          image-tile partition of a channel
+  C5      V_shell(2048) (64-bit addressing: 2050^3 padded voxels), 4096x4096, + the 8-part partition
+C1 (64^3, 256x256, EA only) is checked whole in test_gpu_parity.py / test_gpu_golden.py.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import assert_parity_full_size
+
+pytestmark = pytest.mark.gpu
+
+vr = pytest.importorskip("volume_renderer_amd")
+torch = pytest.importorskip("torch")
+from volume_renderer_amd import mex  # noqa: E402
+
+THREADS = 16  # the GPU box's CPU share (os.cpu_count() there reports the whole host)
+EX1_LIGHTS = np.array([[500, 1000, 550, 0, 1, 1], [0, 550, 90, 1, 0.5, 1]], np.float32)
+EX3_LIGHT = np.array([[-15, 15, 0, 0.5, 0.5, 0.5]], np.float32)
+
+
+@pytest.fixture(autouse=True)
+def _free():
+    yield
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def device_shell(n):
+    t = torch.empty(n ** 3, dtype=torch.float32, device="cuda")
+    mex.synth_shell_device(t.data_ptr(), n)
+    torch.cuda.synchronize()
+    return t
+
+
+def device_structure(n):
+    """The second channel of C4 (example3.m's structure channel): a bounded smooth blob off the
+    centre, zero on the 2-voxel border, generated plane block by plane block in fp32."""
+    t = torch.empty(n ** 3, dtype=torch.float32, device="cuda")
+    c = (torch.arange(n, device="cuda", dtype=torch.float32) + 0.5) / n
+    step = max(1, (1 << 26) // (n * n))
+    for z0 in range(0, n, step):
+        z = c[z0:z0 + step].view(-1, 1, 1)
+        r2 = (c.view(1, 1, -1) - 0.58) ** 2 + (c.view(1, -1, 1) - 0.45) ** 2 + (z - 0.5) ** 2
+        blk = torch.clamp(torch.exp(-r2 / 0.02) - 0.05, min=0.0)  # [z][y][x]: column-major (x fastest)
+        t[z0 * n * n:(z0 + blk.shape[0]) * n * n] = blk.reshape(-1)
+    torch.cuda.synchronize()
+    return t
+
+
+def host(t, dims):
+    return t.cpu().numpy().reshape(dims, order="F")
+
+
+def lights_arg(L):
+    return [vr.LightSource(l[:3], l[3:]) for l in L]
+
+
+def stamped(v, t):
+    v.TimeLastUpdate = np.uint64(t)
+    return v
+
+
+def argv(R, res, props, thr, color, factors, es=(1, 1, 1)):
+    """The positional 'render' arguments after (lights, illumination)."""
+    return (np.float32(factors), np.float32(es), np.uint64(res), np.flip(R, 0).astype(np.float32),
+            np.float32(props), np.float32(thr), np.float32(color))
+
+
+def chords(W, H, R, props, bmax):
+    """Chord length (world units) of every primary ray through the box, [x * H + y] order; the
+    camera of volumeRender_kernel.cu:388-425 in float64."""
+    X, Y, Z = (np.asarray(R, np.float64)[:, i] for i in range(3))
+    xoff, f, dist = (float(p) for p in props)
+    nX = X / np.linalg.norm(X)
+    x = np.arange(W, dtype=np.float64)[:, None]
+    y = np.arange(H, dtype=np.float64)[None, :]
+    r = H / W
+    u = x / W * 2 - 1
+    v = (y / H) * 2 * r - r
+    d = [u * nX[i] + v * Y[i] + f * Z[i] for i in range(3)]
+    nrm = np.sqrt(d[0] ** 2 + d[1] ** 2 + d[2] ** 2)
+    eye = xoff * X - dist * Z
+    tn = np.full((W, H), -np.inf)
+    tf = np.full((W, H), np.inf)
+    for i in range(3):
+        di = d[i] / nrm
+        with np.errstate(divide="ignore", invalid="ignore"):
+            inv = 1.0 / di
+            ta, tb = (-bmax[i] - eye[i]) * inv, (bmax[i] - eye[i]) * inv
+        tn = np.maximum(tn, np.minimum(ta, tb))
+        tf = np.minimum(tf, np.maximum(ta, tb))
+    return np.where(tf > np.maximum(tn, 0), tf - np.maximum(tn, 0), 0.0).reshape(-1)
+
+
+def sample_pixels(img, R, props, bmax, seed, n_rand=6000, n_long=1500, n_lit=1500):
+    """(xs, ys, uniform): uniform pixels + longest chords + brightest product pixels, no repeats;
+    `uniform` marks the uniformly drawn ones (an unbiased sample of the image)."""
+    H, W = img.shape[:2]
+    rng = np.random.default_rng(seed)
+    k_rand = rng.choice(W * H, size=min(n_rand, W * H), replace=False)
+    ch = chords(W, H, R, props, bmax)
+    k_long = np.argpartition(-ch, n_long)[:n_long]
+    lum = np.asarray(img, np.float64).sum(axis=2).T.reshape(-1)  # [x * H + y]
+    k_lit = np.argpartition(-lum, n_lit)[:n_lit]
+    k = np.unique(np.concatenate([k_rand, k_long, k_lit]))
+    assert ch[k_long].min() > 0
+    return k // H, k % H, np.isin(k, k_rand)
+
+
+def oracle_check(S, h, lights, lut, rargs, img, R, props, bmax, what, seed=1):
+    """Check the product image at the stratified pixel sample against the fp32 oracle with its
+    fp64 envelope (conftest.assert_parity_full_size: the SURVEY.md 8c tolerance with the envelope
+    floored at its RMS over the lit sampled channels, as rays of thousands of samples need), on all
+    sampled pixels -- the longest and brightest rays included.  Stats are also given for the
+    uniformly drawn pixels alone (an unbiased sample of the image)."""
+    xs, ys, uni = sample_pixels(img, R, props, bmax, seed)
+    ref32, st32 = S.render(h, lights, lut, *rargs, pixels=(xs, ys), threads=THREADS)
+    ref64, _ = S.render(h, lights, lut, *rargs, pixels=(xs, ys), double=True, threads=THREADS)
+    got = np.ascontiguousarray(np.asarray(img, np.float32)[ys, xs, :])
+    stats = assert_parity_full_size(got, ref32, ref64, what)
+    u = assert_parity_full_size(got[uni], ref32[uni], ref64[uni], what + " (uniform pixels)")
+    stats.update(pixels=int(len(xs)), uniform_pixels=int(uni.sum()), samples=int(st32.sum()),
+                 lit_pixels=float((ref32.max(axis=1) > 0).mean()), uniform_frac_within_survey=u["frac_within_survey"],
+                 uniform_rms_ratio=u["rms_ratio"])
+    print("PARITY", json.dumps(dict(what=what, **stats)))
+    assert stats["samples"] > 100 * len(xs) and ref32.max() > 0
+    return stats
+
+
+def ex1_scene(n, W, H, gradients=False):
+    """The example1.m scene (2 lights, HG LUT 64, Fe 1 Fr 0.4 Fa 0.6, colour [1 1 0], thr 0.9,
+    rotate(125,25,0), f 3, dist 6, reflection = the class default Volume(1)) on V_shell(n) in HBM:
+    product render through the 'render' mex command (production kernels), oracle session on the
+    same voxels."""
+    t = device_shell(n)
+    dims = (n, n, n)
+    em = mex.DeviceVolume(t.data_ptr(), dims, last_update=10, owner=t)
+    refl = stamped(vr.Volume(1), 5)
+    lut = stamped(vr.Volume(vr.HenyeyGreenstein(64)), 7)
+    R = O.rotation(125, 25, 0)
+    rargs = argv(R, [H, W], [0, 3, 6], 0.9, [1, 1, 0], [1, 0.4, 0.6])
+    S = O.OracleSession(copy=False)
+    oh = S.new()
+    hem = host(t, dims)
+    oem = O.OVolume(hem, 10)
+    ore = O.OVolume(np.ones((1, 1), np.float32), 5)
+    h = vr.volumeRender("new")
+    keep = [t]
+    if gradients:
+        g = [torch.empty_like(t) for _ in range(3)]
+        mex.gradient_device(t.data_ptr(), dims, g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr())
+        torch.cuda.synchronize()
+        dv = [mex.DeviceVolume(gi.data_ptr(), dims, last_update=11 + i, owner=gi) for i, gi in enumerate(g)]
+        vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em, *dv)
+        S.sync_volumes(oh, 0, oem, ore, oem, *(O.OVolume(host(gi, dims), 11 + i) for i, gi in enumerate(g)))
+        keep += g
+    else:
+        vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)
+        S.sync_volumes(oh, 0, oem, ore, oem)
+    img = vr.volumeRender("render", h, lights_arg(EX1_LIGHTS), lut, *rargs)
+    olut = O.OVolume(lut.Data, 7)
+    return dict(h=h, S=S, oh=oh, img=img, R=R, rargs=rargs, lut=lut, olut=olut, keep=keep, n=n, W=W, H=H)
+
+
+def partition_check(sc, nparts, bc=16, want_k=None):
+    """The image-tile partition of SURVEY.md 8e on one GPU: every part rendered with the production
+    launch of its shape (depth lanes for a part, longest-first schedule from the second launch of a
+    shape on), assembled on the device, equals the whole frame bit for bit."""
+    W, H = sc["W"], sc["H"]
+    ra, keep = mex.render_args(lights_arg(EX1_LIGHTS), sc["lut"], *sc["rargs"])
+    maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
+    if want_k is not None:
+        assert mex.depth_lanes(maxc, H) == want_k
+    full = np.asarray(sc["img"], np.float32).reshape(-1, order="F")
+    for launch in range(2):  # the first launch measures block durations, the second follows them
+        parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
+        for p in range(nparts):
+            mex.render_device(sc["h"], ra, parts[p].data_ptr(), mex.partition(bc, p, nparts))
+        out = torch.zeros(3 * W * H, dtype=torch.float32, device="cuda")
+        mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32)), (nparts, launch)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("shade", ["fast", "exact"])
+def test_c2_1024x768_compute_gradient(monkeypatch, shade):
+    """C2 with the default (fast) shading arithmetic, and with VR_EXACT_SHADE=1 (the oracle's op
+    sequence)."""
+    if shade == "exact":
+        monkeypatch.setenv("VR_EXACT_SHADE", "1")
+    else:
+        monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
+    sc = ex1_scene(1024, 1024, 768)
+    st = oracle_check(sc["S"], sc["oh"], EX1_LIGHTS, sc["olut"], sc["rargs"], sc["img"], sc["R"], [0, 3, 6],
+                      (1, 1, 1), f"C2 V_shell(1024) 1024x768 {shade}")
+    if shade == "exact":  # only acosf / expf come from another library: much closer than fp32 rounding
+        assert st["rms_ratio"] <= 0.25, st
+    vr.volumeRender("delete", sc["h"])
+
+
+@pytest.mark.timeout(300)
+def test_metric_config_1920x1080():
+    """bench.py's frame (BASELINE.json metric config), whole image through vr_render, the default
+    two depth lanes per ray; and the 8-part partition (one part per GPU of the N=8 scaling run:
+    four depth lanes, longest-first schedule) assembles to it bit for bit."""
+    sc = ex1_scene(1024, 1920, 1080)
+    assert mex.depth_lanes(1920, 1080) == 2
+    oracle_check(sc["S"], sc["oh"], EX1_LIGHTS, sc["olut"], sc["rargs"], sc["img"], sc["R"], [0, 3, 6], (1, 1, 1),
+                 "metric V_shell(1024) 1920x1080")
+    partition_check(sc, 8, want_k=4)
+    vr.volumeRender("delete", sc["h"])
+
+
+@pytest.mark.timeout(300)
+def test_c3_lookup_gradient_1920x1080():
+    """example1_grad.m path: three precomputed gradient volumes resident with the emission (16 GiB),
+    the march reads their interleaved copy."""
+    sc = ex1_scene(1024, 1920, 1080, gradients=True)
+    oracle_check(sc["S"], sc["oh"], EX1_LIGHTS, sc["olut"], sc["rargs"], sc["img"], sc["R"], [0, 3, 6], (1, 1, 1),
+                 "C3 lookup V_shell(1024) 1920x1080")
+    vr.volumeRender("delete", sc["h"])
+
+
+@pytest.mark.timeout(400)
+def test_c5_2048_cube_4096_squared():
+    """V_shell(2048) (32 GiB; 2050^3 padded voxels > 2^32: the 64-bit addressing path), 4096x4096,
+    HG 2 lights, on-the-fly gradient; and the 8-part partition of the C5 8-GPU config."""
+    sc = ex1_scene(2048, 4096, 4096)
+    oracle_check(sc["S"], sc["oh"], EX1_LIGHTS, sc["olut"], sc["rargs"], sc["img"], sc["R"], [0, 3, 6], (1, 1, 1),
+                 "C5 V_shell(2048) 4096x4096")
+    partition_check(sc, 8)
+    vr.volumeRender("delete", sc["h"])
+
+
+@pytest.mark.timeout(400)
+def test_c4_two_channels_stereo_1920x1080():
+    """example3.m: a main channel (V_shell(1024), colour [1 1 1], Fe = Fa = Fr = 1) and a structure
+    channel (a second field, colour [0 1 0], Fe 0.5) with one light, LUT 64, thr 0.95, f 4.5,
+    rotate(90,0,0) then rotate(-15,15,15), off-axis stereo CameraXOffset 0.06 (both eyes at
+    1920 + delta columns before the crop) -- all four views marched by vr_render_channels.  Each
+    channel x eye is checked against its own oracle session (the reference renders the channels
+    one after the other, each right after its sync).  The 4-GPU split of the config: a channel's
+    view rendered as a 4-part partition assembles to the fused launch's image bit for bit."""
+    n, W, H = 1024, 1920, 1080
+    R = O.rotation(-15, 15, 15, R=O.rotation(90, 0, 0))
+    f, dist, xoff = 4.5, 6.0, 0.06
+    base = xoff / 2
+    fov = 2 * np.arctan(1 / f)
+    delta = base * W / (2 * f * np.tan(fov / 2))
+    delta = int(np.floor(abs(delta) + 0.5))
+    res = [H, W + delta]
+    lut = stamped(vr.Volume(vr.HenyeyGreenstein(64)), 7)
+    refl = stamped(vr.Volume(1), 5)
+    chans, oracles, keep = [], [], []
+    for i, (gen, color, fe) in enumerate(((device_shell, [1, 1, 1], 1.0), (device_structure, [0, 1, 0], 0.5))):
+        t = gen(n)
+        keep.append(t)
+        em = mex.DeviceVolume(t.data_ptr(), (n, n, n), last_update=20 + i, owner=t)
+        h = vr.volumeRender("new")
+        rl = argv(R, res, [-base, f, dist], 0.95, color, [fe, 1, 1])
+        chans.append((h, np.uint64(0), [em, refl, em], (lights_arg(EX3_LIGHT), lut) + rl))
+        S = O.OracleSession(copy=False)
+        oh = S.new()
+        oem = O.OVolume(host(t, (n, n, n)), 20 + i)
+        S.sync_volumes(oh, 0, oem, O.OVolume(np.ones((1, 1), np.float32), 5), oem)
+        oracles.append((S, oh, color, fe))
+    out = mex.render_channels(chans, stereo=True, base=np.float32(base))
+    olut = O.OVolume(lut.Data, 7)
+    for i, ((left, right), (S, oh, color, fe)) in enumerate(zip(out, oracles)):
+        for img, off, eye in ((left, -base, "left"), (right, base, "right")):
+            assert img.shape == (H, W + delta, 3)
+            rargs = argv(R, res, [off, f, dist], 0.95, color, [fe, 1, 1])
+            oracle_check(S, oh, EX3_LIGHT, olut, rargs, img, R, [off, f, dist], (1, 1, 1),
+                         f"C4 channel {i} {eye} eye", seed=10 + 2 * i + (eye == "right"))
+    # the 4-GPU image-tile split: channel 0's left view, production part launches (re-synced: the
+    # textures are module-global and the structure channel was synced last)
+    h0 = chans[0][0]
+    vr.volumeRender("sync_volumes", h0, np.uint64(0), *chans[0][2])
+    sc = dict(h=h0, W=W + delta, H=H, img=out[0][0], lut=lut, rargs=argv(R, res, [-base, f, dist], 0.95, [1, 1, 1],
+                                                                         [1.0, 1, 1]))
+    ra, k2 = mex.render_args(lights_arg(EX3_LIGHT), lut, *sc["rargs"])
+    Wd, bc, nparts = W + delta, 16, 4
+    maxc = max(mex.partition_columns(Wd, mex.partition(bc, p, nparts)) for p in range(nparts))
+    full = np.asarray(out[0][0], np.float32).reshape(-1, order="F")
+    for launch in range(2):
+        parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
+        for p in range(nparts):
+            mex.render_device(h0, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts))
+        o = torch.zeros(3 * Wd * H, dtype=torch.float32, device="cuda")
+        mex.assemble_partitions(parts.data_ptr(), Wd, H, bc, nparts, maxc, o.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), full.view(np.uint32)), launch
+    for c in chans:
+        vr.volumeRender("delete", c[0])
+
+
+def test_metric_config_depth_lanes_and_counts(monkeypatch):
+    """Size-independent properties of the metric frame with the production kernels: one, two (the
+    default) and four depth lanes per ray give the same image bit for bit (no sample counter in
+    those launches -- the counter variant is a separate K = 1 launch), and the sample count of the
+    counter launch is that of the 8-part partition's counted launches added up."""
+    n, W, H = 1024, 1920, 1080
+    t = device_shell(n)
+    em = mex.DeviceVolume(t.data_ptr(), (n, n, n), last_update=10, owner=t)
+    refl = stamped(vr.Volume(1), 5)
+    lut = stamped(vr.Volume(vr.HenyeyGreenstein(64)), 7)
+    h = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)
+    del t, em
+    R = O.rotation(125, 25, 0)
+    ra, keep = mex.render_args(lights_arg(EX1_LIGHTS), lut, *argv(R, [H, W], [0, 3, 6], 0.9, [1, 1, 0], [1, 0.4, 0.6]))
+    imgs = {}
+    for k in ("", "1", "2", "4"):
+        if k:
+            monkeypatch.setenv("VR_DEPTH_LANES", k)
+        else:
+            monkeypatch.delenv("VR_DEPTH_LANES", raising=False)
+        assert mex.depth_lanes(W, H) == (int(k) if k else 2)
+        out = torch.zeros(3 * W * H, dtype=torch.float32, device="cuda")
+        mex.render_device(h, ra, out.data_ptr())
+        torch.cuda.synchronize()
+        imgs[k] = out.cpu().numpy()
+    monkeypatch.delenv("VR_DEPTH_LANES")
+    full = imgs[""]
+    assert np.isfinite(full).all() and full.max() > 0
+    for k in ("1", "2", "4"):
+        assert np.array_equal(full.view(np.uint32), imgs[k].view(np.uint32)), k
+    out = torch.zeros(3 * W * H, dtype=torch.float32, device="cuda")
+    steps = torch.zeros(48, dtype=torch.int64, device="cuda")
+    mex.render_device(h, ra, out.data_ptr(), None, steps.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32))
+    total = int(steps[0].item())
+    assert total > 5 * 10 ** 9
+    nparts, bc = 8, 16
+    maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
+    parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
+    psteps = torch.zeros((nparts, 48), dtype=torch.int64, device="cuda")
+    for p in range(nparts):
+        mex.render_device(h, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts), psteps[p].data_ptr())
+    torch.cuda.synchronize()
+    assert int(psteps[:, 0].sum().item()) == total
+    vr.volumeRender("delete", h)

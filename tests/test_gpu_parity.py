@@ -648,57 +648,3 @@ def test_channels_device_images_and_fp32_sum(counter_clock):
     assert np.array_equal(s.cpu().numpy().view(np.uint32), want.view(np.uint32))
     for r in hr + dr:
         r.delete()
-
-
-def test_metric_config_full_size_properties(monkeypatch, counter_clock):
-    """BASELINE.json's metric config at full size (V_shell(1024) in HBM, 1920x1080, HG 2 lights,
-    on-the-fly gradient; bench.py's frame), where the oracle is too slow for a whole image (bench.py
-    checks sampled columns against it): size-independent properties.  One depth lane and two give
-    the same image bit for bit and the same sample count; the 8-rank column partition (the N=8
-    scaling config) assembles to the full image bit for bit and its sample counts add up."""
-    import torch
-    from volume_renderer_amd import mex
-    n, W, H = 1024, 1920, 1080
-    vol = torch.empty(n * n * n, dtype=torch.float32, device="cuda")
-    mex.synth_shell_device(vol.data_ptr(), n)
-    torch.cuda.synchronize()
-    em = mex.DeviceVolume(vol.data_ptr(), (n, n, n), last_update=10, owner=vol)
-    refl = vr.Volume(1)
-    refl.TimeLastUpdate = np.uint64(5)
-    lut = vr.Volume(vr.HenyeyGreenstein(64))
-    lut.TimeLastUpdate = np.uint64(7)
-    lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
-    h = vr.volumeRender("new")
-    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)
-    del vol
-    from volume_renderer_amd.volume_render import _cosd, _sind
-    ca, sa, cb, sb = _cosd(125), _sind(125), _cosd(25), _sind(25)  # rotate(125, 25, 0) as bench.py
-    R = np.array([[1, 0, 0], [0, ca, -sa], [0, sa, ca]]) @ np.array([[cb, 0, sb], [0, 1, 0], [-sb, 0, cb]])
-    ra, keep = mex.render_args(lights, lut, np.float32([1.0, 0.4, 0.6]), np.float32([1, 1, 1]),
-                               np.uint64([H, W]), np.flip(R, 0).astype(np.float32),
-                               np.float32([0, 3.0, 6.0]), np.float32(0.9), np.float32([1, 1, 0]))
-    imgs, samples = {}, {}
-    for k in ("1", "2"):
-        monkeypatch.setenv("VR_DEPTH_LANES", k)
-        out = torch.zeros(3 * W * H, dtype=torch.float32, device="cuda")
-        steps = torch.zeros(48, dtype=torch.int64, device="cuda")
-        mex.render_device(h, ra, out.data_ptr(), None, steps.data_ptr())
-        torch.cuda.synchronize()
-        imgs[k], samples[k] = out.cpu().numpy(), int(steps[0].item())
-    monkeypatch.delenv("VR_DEPTH_LANES")
-    full = imgs["1"]
-    assert np.isfinite(full).all() and full.max() > 0 and samples["1"] > 10 ** 9
-    assert np.array_equal(full.view(np.uint32), imgs["2"].view(np.uint32))
-    assert samples["1"] == samples["2"]
-    nparts, bc = 8, 16
-    maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
-    parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
-    steps = torch.zeros((nparts, 48), dtype=torch.int64, device="cuda")
-    for p in range(nparts):
-        mex.render_device(h, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts), steps[p].data_ptr())
-    out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
-    mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
-    torch.cuda.synchronize()
-    assert np.array_equal(out.cpu().numpy().reshape(-1).view(np.uint32), full.view(np.uint32))
-    assert int(steps[:, 0].sum().item()) == samples["1"]
-    vr.volumeRender("delete", h)

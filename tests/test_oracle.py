@@ -208,3 +208,5 @@ def test_golden_fixtures(name):
     img, steps = G.CASES[name]()
     assert int(data["steps"]) == steps
     assert np.array_equal(img.view(np.uint32), data["image"].view(np.uint32))
+    img64, _ = G.oracle_render(name, double=True)
+    assert np.array_equal(img64.view(np.uint32), data["image64"].view(np.uint32))

@@ -1048,10 +1048,16 @@ static int do_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_
                     const vr_volume *dy, const vr_volume *dz) {
   if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
   if (!emission || !reflection || !absorption) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
-  const bool lookup = dx && dy && dz;
-  if (!lookup && (dx || dy || dz))
-    return fail(VR_ERR_ARGUMENT, "All gradient dimensions need to be set and of type Volume!");
-  for (const vr_volume *v : {emission, reflection, absorption, dx, dy, dz}) {
+  // render.cpp:105-113 keys on the argument count: 9 takes the gradient volumes (lookup), 6 resets
+  // them, 7 or 8 (dx or dx, dy given, the rest NULL) keeps the handle's previous gradient volumes
+  // without reading the given ones; setGradientMethod(compute) then MManager::sync re-enters lookup
+  // mode if kept gradient volumes exist (mmanager.hxx:193-200).
+  const int given = (dx != nullptr) + (dy != nullptr) + (dz != nullptr);
+  const bool lookup = given == 3;
+  if (!lookup && given && !(dx && (dy || !dz)))
+    return fail(VR_ERR_ARGUMENT, "sync_volumes: gradient volumes must be given in order (dx, dy, dz)");
+  for (const vr_volume *v : {emission, reflection, absorption, lookup ? dx : nullptr, lookup ? dy : nullptr,
+                             lookup ? dz : nullptr}) {
     if (!v) continue;
     const uint64_t n = v->dims[0] * v->dims[1] * v->dims[2];
     if (n && !v->data) return fail(VR_ERR_ARGUMENT, "volume data is NULL");
@@ -1069,7 +1075,7 @@ static int do_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_
     h->vol[T_DX] = make_rec(dx);
     h->vol[T_DY] = make_rec(dy);
     h->vol[T_DZ] = make_rec(dz);
-  } else {
+  } else if (given == 0) {
     reset_gradients(h);
   }
   required += required_memory(h);

@@ -325,8 +325,10 @@ def volumeRender(cmd, *args):
         elif nrhs == 6:
             check(L.vr_sync_volumes(h, t_sync, ctypes.byref(em), ctypes.byref(re), ctypes.byref(ab),
                                     None, None, None))
-        else:
-            raise _lib.VrError(5, "sync_volumes: expected 6 or 9 arguments")
+        else:  # 7, 8 or > 9 arguments: the previous gradient volumes are kept (render.cpp:105-113)
+            flag = VrVolume()  # not read: only its presence selects the form
+            check(L.vr_sync_volumes(h, t_sync, ctypes.byref(em), ctypes.byref(re), ctypes.byref(ab),
+                                    ctypes.byref(flag), ctypes.byref(flag) if nrhs != 7 else None, None))
         if nrhs > 9:
             warnings.warn("SyncVolumes: Unexpected arguments ignored.")
         return None
