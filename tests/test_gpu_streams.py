@@ -1,0 +1,103 @@
+"""Renders in flight on several streams while the host changes what the next render reads
+(vr_resources.h): per-launch light lists, a changed illumination LUT and a re-uploaded volume must
+never reach a launch that was issued before the change.  Every image is compared bit for bit with
+the same frame rendered alone (the reference serialises everything, so that is its output)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+vr = pytest.importorskip("volume_renderer_amd")
+torch = pytest.importorskip("torch")
+from volume_renderer_amd import mex  # noqa: E402
+
+R = np.flip(O.rotation(125, 25, 0), 0).astype(np.float32)
+
+
+def _stamped(data, t):
+    v = vr.Volume(data)
+    v.TimeLastUpdate = np.uint64(t)
+    return v
+
+
+def _args(lights, lut, res):
+    return (lights, lut, np.float32([1, 0.4, 0.6]), np.float32([1, 1, 1]), np.uint64(res), R,
+            np.float32([0, 3, 6]), np.float32(0.9), np.float32([1, 1, 0]))
+
+
+LIGHTS_A = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+LIGHTS_B = [vr.LightSource([-300, 200, 800], [1, 0.2, 0.1])]
+
+
+def test_light_lists_and_luts_alternating_across_streams():
+    """Frames alternating two light lists (2 lights / 1 light) and two LUTs, issued round-robin on
+    three streams without waiting: each equals its serial render."""
+    em = _stamped(O.shell_volume(96), 11)
+    re = _stamped(np.float32(1.0), 12)
+    luts = [_stamped(vr.HenyeyGreenstein(32, 0.8), 13), _stamped(vr.HenyeyGreenstein(32, 0.3), 14)]
+    res = (384, 512)
+    h = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, re, em)
+    variants = [(LIGHTS_A, luts[0]), (LIGHTS_B, luts[1]), (LIGHTS_B, luts[0]), (LIGHTS_A, luts[1])]
+    serial = [vr.volumeRender("render", h, *_args(l, lut, res)) for l, lut in variants]
+    for a in serial:
+        assert a.max() > 0
+    assert not np.array_equal(serial[0], serial[1])
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    H, W = res
+    outs, keep = [], []
+    for k in range(12):
+        l, lut = variants[k % 4]
+        ra, kp = mex.render_args(*_args(l, lut, res))
+        keep.append(kp)
+        o = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+        mex.render_device(h, ra, o.data_ptr(), None, 0, streams[k % 3].cuda_stream)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for k, o in enumerate(outs):
+        want = serial[k % 4].reshape(-1, order="F")
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32)), k
+    vr.volumeRender("delete", h)
+
+
+@pytest.mark.parametrize("device_data", [False, True])
+def test_volume_upload_while_previous_frame_renders(device_data):
+    """A movie frame whose volume changed: 'sync_volumes' uploads the new data (host array or device
+    tensor) while the previous frame's render is still running on another stream; both frames
+    equal their serial renders (the in-flight frame keeps its buffer until it completes)."""
+    n, res = 160, (600, 800)
+    data = [O.shell_volume(n), np.asfortranarray(O.shell_volume(n)[::-1, :, ::-1] * np.float32(0.8))]
+    lut = _stamped(vr.HenyeyGreenstein(32), 5)
+    re = _stamped(np.float32(1.0), 6)
+    H, W = res
+    h = vr.volumeRender("new")
+
+    def volume(k):
+        if device_data:
+            t = torch.from_numpy(data[k % 2].reshape(-1, order="F").copy()).cuda()
+            return mex.DeviceVolume(t.data_ptr(), (n, n, n), last_update=100 + k, owner=t)
+        return _stamped(data[k % 2], 100 + k)
+
+    serial = []
+    for k in range(2):
+        v = volume(k)
+        vr.volumeRender("sync_volumes", h, np.uint64(1), v, re, v)
+        serial.append(vr.volumeRender("render", h, *_args(LIGHTS_A, lut, res)))
+    assert not np.array_equal(serial[0], serial[1])
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs, vols = [], []
+    for k in range(6):
+        v = volume(k)
+        vols.append(v)
+        vr.volumeRender("sync_volumes", h, np.uint64(1), v, re, v)  # while frame k-1 may still run
+        ra, kp = mex.render_args(*_args(LIGHTS_A, lut, res))
+        o = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+        mex.render_device(h, ra, o.data_ptr(), None, 0, streams[k % 2].cuda_stream)
+        outs.append((o, kp))
+    torch.cuda.synchronize()
+    for k, (o, _) in enumerate(outs):
+        want = serial[k % 2].reshape(-1, order="F")
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32)), k
+    vr.volumeRender("delete", h)

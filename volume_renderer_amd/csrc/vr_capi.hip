@@ -29,6 +29,7 @@
 
 #include "../../include/vrhip.h"
 #include "vr_device.h"
+#include "vr_resources.h"
 
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
@@ -137,15 +138,10 @@ struct DevBuf {
   // the MATLAB Volume it was uploaded from (VolRec identity: data pointer, TimeLastUpdate, size)
   const float *src_data = nullptr;
   uint64_t src_last_update = 0, src_bytes = 0;
-  ~DevBuf() {
-    if (ptr) {
-      int cur = 0;
-      (void)hipGetDevice(&cur);
-      (void)hipSetDevice(device);
-      (void)hipFree(ptr);
-      (void)hipSetDevice(cur);
-    }
-  }
+  // completion of the last launch that reads it (vr_resources.h): it is neither rewritten nor freed
+  // before then
+  vr_host::EventPtr last_use;
+  ~DevBuf() { vr_host::pooled_free(ptr, bytes, device, last_use); }
 };
 using BufPtr = std::shared_ptr<DevBuf>;
 
@@ -169,9 +165,6 @@ struct vr_context {
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
-  void *d_views = nullptr;
-  size_t d_views_bytes = 0;
-  std::vector<unsigned char> h_views;  // host image of d_views (alive until the copy has run)
   float *d_chan = nullptr;             // per-view images of the host entry
   size_t d_chan_bytes = 0;
   // the module-global texture bindings as this handle's last sync left them (vr_render_channels
@@ -190,10 +183,8 @@ struct TexUnit {
   BufPtr bind[T_COUNT];
   int32_t idx_em = T_EM, idx_ab = T_EM, idx_re = T_RE;  // kernel.cu:75-85
   int32_t grad_method = G_COMPUTE;                       // kernel.cu:55
-  std::vector<vr::DevLight> lights;                      // c_numLightSources = lights.size()
-  vr::DevLight *d_lights = nullptr;
-  size_t d_lights_cap = 0;
-  int d_lights_device = 0;
+  std::vector<vr::DevLight> lights;                      // c_numLightSources = lights.size(); staged
+                                                         // per launch (vr_host::LaunchRec::stage)
   // lookup gradient, interleaved (gx, gy, gz, 0) per padded voxel, built from the bound gradient
   // textures when their dims equal the emission's; rebuilt when any of them changes
   std::shared_ptr<DevBuf> gvec;
@@ -226,15 +217,6 @@ void reset_tex_unit() {
   g_tex.idx_re = T_RE;
   g_tex.grad_method = G_COMPUTE;
   g_tex.lights.clear();
-  if (g_tex.d_lights) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    (void)hipSetDevice(g_tex.d_lights_device);
-    (void)hipFree(g_tex.d_lights);
-    (void)hipSetDevice(cur);
-  }
-  g_tex.d_lights = nullptr;
-  g_tex.d_lights_cap = 0;
 }
 
 bool valid(vr_context *h) { return h && g_contexts.count(h) && h->signature == 0xFF00F0A5u; }
@@ -249,46 +231,34 @@ bool env_flag_off(const char *name) {
 }
 
 // syncVolume (kernel.cu:659-672): unbind the texture, drop the old array, upload the volume into a
-// fresh device buffer and bind it.  A buffer nobody else references is overwritten in place.
+// device buffer and bind it.  The handle's previous buffer of the slot is rewritten in place when
+// nothing else holds it and no launch still reads it; otherwise a fresh buffer is taken and the old
+// one is freed when its last launch completes (a render of the previous frame may be in flight on
+// another stream while this frame's volumes upload, vr_resources.h).
 void sync_volume(vr_context *h, int tex, int slot) {
   g_tex.bind[tex].reset();
   const VolRec &v = h->vol[slot];
   const uint64_t n = v.dims[0] * v.dims[1] * v.dims[2];
   const uint64_t padded = n ? (v.dims[0] + 2) * (v.dims[1] + 2) * (v.dims[2] + 2) * sizeof(float) : 0;
   BufPtr b = h->buf[slot];
-  if (!(b && b.use_count() == 1 && b->bytes == padded && b->device == h->device)) {
+  if (!(b && b.use_count() == 2 && b->bytes == padded && b->device == h->device && vr_host::done(b->last_use))) {
     h->buf[slot].reset();
     b = std::make_shared<DevBuf>();
     b->device = h->device;
     b->bytes = padded;
-    if (padded) VR_HIP(hipMalloc(&b->ptr, padded));
+    if (padded) VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->ptr), padded, h->device));
   }
   for (int i = 0; i < 3; ++i) b->dims[i] = v.dims[i];
   b->nonfinite = false;
   b->maxabs = 0.f;
+  b->last_use.reset();
   if (n) {
     if (!v.data) throw HipError{hipErrorInvalidValue, "volume data is NULL"};
-    const float *src = v.data;
-    float *staging = nullptr;
-    if (v.location != VR_DEVICE) {  // H2D into a dense staging buffer, then pad on the device
-      VR_HIP(hipMalloc(&staging, n * sizeof(float)));
-      hipError_t e = hipMemcpy(staging, v.data, n * sizeof(float), hipMemcpyHostToDevice);
-      if (e != hipSuccess) {
-        (void)hipFree(staging);
-        throw HipError{e, "hipMemcpy (volume upload)"};
-      }
-      src = staging;
-    }
-    vr::BufStats *d_st = nullptr;
+    vr_host::Uploader &U = vr_host::uploaders()[h->device];
+    VR_HIP(U.init(h->device));
     vr::BufStats st{0u, 0.f};
-    hipError_t e = hipMalloc(&d_st, sizeof(vr::BufStats));
-    if (e == hipSuccess) e = hipMemset(d_st, 0, sizeof(vr::BufStats));
-    if (e == hipSuccess) e = vr::launch_pad(src, b->ptr, (int32_t)v.dims[0], (int32_t)v.dims[1], (int32_t)v.dims[2], nullptr);
-    if (e == hipSuccess) e = vr::launch_stats(src, n, d_st, nullptr);
-    if (e == hipSuccess) e = hipMemcpy(&st, d_st, sizeof(st), hipMemcpyDeviceToHost);
-    if (staging) (void)hipFree(staging);
-    if (d_st) (void)hipFree(d_st);
-    if (e != hipSuccess) throw HipError{e, "volume upload (pad/stats)"};
+    VR_HIP(U.upload(v.data, v.location == VR_DEVICE, (int32_t)v.dims[0], (int32_t)v.dims[1], (int32_t)v.dims[2],
+                    b->ptr, &st));
     b->nonfinite = st.nonfinite != 0;
     b->maxabs = st.maxabs;
   }
@@ -382,6 +352,12 @@ uint64_t required_memory(const vr_context *h) {
 // MManager::checkFreeDeviceMemory (mmanager.hxx:144-173)
 int check_free_device_memory(uint64_t required) {
   size_t free_b = 0, total_b = 0;
+  VR_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (free_b >= required) return VR_OK;
+  int dev = 0;  // pooled / retired buffers are free memory to MATLAB's eyes: release them, recheck
+  VR_HIP(hipGetDevice(&dev));
+  vr_host::pool_clear(dev);
+  vr_host::prune_retired(true);
   VR_HIP(hipMemGetInfo(&free_b, &total_b));
   if (free_b >= required) return VR_OK;
   std::ostringstream os;
@@ -547,7 +523,7 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
   P.gz = dev_tex(g_tex.bind[T_DZ]);
   P.lut = dev_tex(g_tex.bind[T_LIGHT]);
   P.num_lights = (int32_t)g_tex.lights.size();
-  P.lights = g_tex.d_lights;
+  P.lights = nullptr;  // staged per launch on the launch's stream (stage_frame)
   F.mode = P.num_lights == 0 ? 0 : (g_tex.grad_method == G_LOOKUP ? 2 : 1);
   F.ab_alias = same_tex(P.ab, P.em);
   const bool em_grid = P.em.p && !P.em.one;  // the centre sample computes its three axes
@@ -620,17 +596,23 @@ void upload_lights(vr_context *h, const vr_render_args *a) {
     g_tex.lights[l] = vr::DevLight{L.position[2], L.position[1], L.position[0], L.color[0], L.color[1],
                                    L.color[2]};
   }
-  if (n > g_tex.d_lights_cap || g_tex.d_lights_device != h->device) {
-    if (g_tex.d_lights) (void)hipFree(g_tex.d_lights);
-    g_tex.d_lights = nullptr;
-    g_tex.d_lights_cap = 0;
-    VR_HIP(hipMalloc(&g_tex.d_lights, std::max<size_t>(n, 8) * sizeof(vr::DevLight)));
-    g_tex.d_lights_cap = std::max<size_t>(n, 8);
-    g_tex.d_lights_device = h->device;
-  }
-  if (n) VR_HIP(hipMemcpy(g_tex.d_lights, g_tex.lights.data(), n * sizeof(vr::DevLight), hipMemcpyHostToDevice));
   h->vol[T_LIGHT] = make_rec(a->illumination);
   sync_volume_if_changed(h, T_LIGHT, T_LIGHT);
+}
+
+// What a launch reads (vr_resources.h): every bound texture buffer (and the interleaved lookup
+// gradient) is marked with the launch's completion event by finish(); the frame's light list is
+// staged on the launch stream.
+using LaunchRec = vr_host::LaunchRec<BufPtr>;
+void bind_reads(LaunchRec &L) {
+  for (const BufPtr &b : g_tex.bind)
+    if (b) L.reads.push_back(b);
+  if (g_tex.gvec) L.reads.push_back(g_tex.gvec);
+}
+void stage_frame(LaunchRec &L, vr::RenderParams &P, const std::vector<vr::DevLight> &lights) {
+  const void *d = nullptr;
+  VR_HIP(L.stage(lights.data(), lights.size() * sizeof(vr::DevLight), &d));
+  P.lights = static_cast<const vr::DevLight *>(d);
 }
 
 int64_t part_columns(int64_t w, int32_t bc, int32_t part, int32_t np) {
@@ -658,9 +640,6 @@ void set_chunk_halo(Frame &F, int K) {
 }
 
 void free_views(vr_context *h) {
-  if (h->d_views) (void)hipFree(h->d_views);
-  h->d_views = nullptr;
-  h->d_views_bytes = 0;
   if (h->d_chan) (void)hipFree(h->d_chan);
   h->d_chan = nullptr;
   h->d_chan_bytes = 0;
@@ -782,7 +761,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
       gv->bytes = n * 4 * sizeof(float);
-      if (hipMalloc(&gv->ptr, gv->bytes) == hipSuccess) {
+      if (vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device) == hipSuccess) {
         VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
         g_tex.gvec = gv;
         for (int i = 0; i < 3; ++i) {
@@ -800,6 +779,11 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     *fusable = 1;
     return VR_OK;
   }
+  LaunchRec L;
+  L.stream = stream;
+  L.device = h->device;
+  bind_reads(L);
+  stage_frame(L, P, g_tex.lights);
   if (march) {
     const int K = P.steps ? 1 : depth_lanes(P);  // the counter variant exists for K = 1
     set_chunk_halo(F, K);
@@ -878,6 +862,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
     }
   }
+  VR_HIP(L.finish());
   return VR_OK;
 }
 
@@ -945,7 +930,13 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   static const slab_fn sfns[2][3] = {
       {vr::exact::launch_march_slab_k1, vr::exact::launch_march_slab_k2, vr::exact::launch_march_slab_k4},
       {vr::fast::launch_march_slab_k1, vr::fast::launch_march_slab_k2, vr::fast::launch_march_slab_k4}};
+  LaunchRec L;
+  L.stream = stream;
+  L.device = h->device;
+  bind_reads(L);
+  stage_frame(L, P, g_tex.lights);
   VR_HIP(sfns[P.fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](P, F.mode, stream));
+  VR_HIP(L.finish());
   return VR_OK;
 }
 
@@ -997,6 +988,10 @@ int vr_delete(vr_context *h) {
   g_contexts.erase(h);
   h->signature = 0;
   delete h;
+  // cudaDeviceReset waits for and drops everything: so do the retired buffers here
+  (void)hipDeviceSynchronize();
+  vr_host::prune_retired(true);
+  vr_host::pool_clear();
   return VR_OK;
   VR_GUARD_END
 }
@@ -1006,6 +1001,7 @@ int vr_mem_info(vr_context *h, char *buf, size_t buflen) {
   if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   size_t free_b = 0, total_b = 0;
   VR_HIP(hipMemGetInfo(&free_b, &total_b));
   const VolRec &em = h->vol[T_EM], &ab = h->vol[T_AB], &re = h->vol[T_RE];
@@ -1024,7 +1020,8 @@ int vr_mem_info(vr_context *h, char *buf, size_t buflen) {
      << "\t\tdX (MB): " << mb(h->vol[T_DX].memory_size) << " ptr: " << ptr(T_DX) << "\n"
      << "\t\tdY (MB): " << mb(h->vol[T_DY].memory_size) << " ptr: " << ptr(T_DY) << "\n"
      << "\t\tdZ (MB): " << mb(h->vol[T_DZ].memory_size) << " ptr: " << ptr(T_DZ) << "\n"
-     << "\t\tlight (MB): " << mb(h->vol[T_LIGHT].memory_size) << " ptr: " << ptr(T_LIGHT) << "\n\n"
+     << "\t\tlight (MB): " << mb(h->vol[T_LIGHT].memory_size) << " ptr: " << ptr(T_LIGHT) << "\n"
+     << "\t\treusable buffers (MB): " << mb(vr_host::pool_bytes(h->device)) << "\n\n"
      << "\t\tSimilarity of Volumes\n\t\t---------------------\n"
      << "\t\t\tEm\tAb\tRe\n"
      << "\t\tEm\t1\t\n"
@@ -1066,6 +1063,7 @@ static int do_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_
   }
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   uint64_t required = required_memory(h);  // render.cpp:90 (before the new volumes are recorded)
   h->time_last_mem_sync = time_last_mem_sync;
   h->vol[T_EM] = make_rec(emission);
@@ -1082,8 +1080,7 @@ static int do_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_
   int rc = check_free_device_memory(required);
   if (rc) return rc;
   g_tex.grad_method = lookup ? G_LOOKUP : G_COMPUTE;  // setGradientMethod (render.cpp:121)
-  mm_sync(h);
-  VR_HIP(hipDeviceSynchronize());
+  mm_sync(h);  // returns with the volumes resident (vr_host::Uploader); renders in flight keep running
   for (int t = 0; t < T_COUNT; ++t) h->snap_bind[t] = g_tex.bind[t];
   h->snap_idx[0] = g_tex.idx_em;
   h->snap_idx[1] = g_tex.idx_ab;
@@ -1187,21 +1184,14 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
     return ((vmode[k] * 2 + vab[k]) * 2 + views[k].wide_slot) * 2 + views[k].fast_shade;
   };
   std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return key(x) < key(y); });
-  vr_context *h0 = ch[0].handle;
-  // the views' lights in device memory (the global light buffer holds the last channel's only)
-  const size_t bytes = std::max<size_t>(lights.size(), 1) * sizeof(vr::DevLight);
-  if (bytes > h0->d_views_bytes) {
-    if (h0->d_views) VR_HIP(hipFree(h0->d_views));
-    h0->d_views = nullptr;
-    h0->d_views_bytes = 0;
-    VR_HIP(hipMalloc(&h0->d_views, bytes));
-    h0->d_views_bytes = bytes;
-  }
-  vr::DevLight *d_lights = static_cast<vr::DevLight *>(h0->d_views);
-  // the last sync waited for the device, so no earlier launch still reads d_views
-  h0->h_views.assign(bytes, 0);
-  if (!lights.empty()) std::memcpy(h0->h_views.data(), lights.data(), lights.size() * sizeof(vr::DevLight));
-  VR_HIP(hipMemcpyAsync(h0->d_views, h0->h_views.data(), bytes, hipMemcpyHostToDevice, stream));
+  // the views' lights, staged for these launches on their stream (each channel's own list)
+  LaunchRec L;
+  L.stream = stream;
+  L.device = ch[0].handle->device;
+  L.reads = std::move(keep);
+  const void *dl = nullptr;
+  VR_HIP(L.stage(lights.data(), lights.size() * sizeof(vr::DevLight), &dl));
+  const vr::DevLight *d_lights = static_cast<const vr::DevLight *>(dl);
   typedef hipError_t (*views_fn)(const vr::RenderViews &, uint32_t, int, bool, hipStream_t);
   static const views_fn vfns[2][3] = {
       {vr::exact::launch_march_views_k1, vr::exact::launch_march_views_k2, vr::exact::launch_march_views_k4},
@@ -1219,18 +1209,16 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
       vr::RenderParams &P = V.p[k - g0];
       P = views[order[k]];
       for (int d = 0; d < 3; ++d) P.tap_off[d] += (float)(chunk_samples(K) * drift[order[k]][d]);
-      P.lights = d_lights + loff[order[k]];
+      P.lights = d_lights ? d_lights + loff[order[k]] : nullptr;
     }
     const size_t v0 = order[g0];
     VR_HIP(vfns[views[v0].fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](V, (uint32_t)(g1 - g0), vmode[v0],
                                                                               vab[v0] != 0, stream));
     g0 = g1;
   }
-  // a prepared frame's buffer that no handle or binding holds any more is freed on return: wait for
-  // the launches first (the handles' own buffers stay alive, the launches stay asynchronous)
-  bool orphan = false;
-  for (const BufPtr &b : keep) orphan = orphan || b.use_count() == 1;
-  if (orphan) VR_HIP(hipStreamSynchronize(stream));
+  // a prepared frame's buffer that no handle or binding holds any more is freed when these launches
+  // complete (vr_host::free_when_done); the launches stay asynchronous
+  VR_HIP(L.finish());
   return VR_OK;
 }
 
@@ -1240,6 +1228,7 @@ int vr_render_channels_device(const vr_channel *ch, int32_t n, int32_t stereo, f
   if (!ch || n < 1 || !valid(ch[0].handle)) return fail(VR_ERR_HANDLE, "Handle not valid.");
   VR_GUARD_BEGIN
   DeviceGuard dg(ch[0].handle->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   return do_render_channels(ch, n, stereo, base, d_out, (hipStream_t)stream);
   VR_GUARD_END
 }
@@ -1251,6 +1240,7 @@ int vr_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, float ba
   VR_GUARD_BEGIN
   vr_context *h = ch[0].handle;
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   const size_t img = (size_t)ch[0].args->resolution[0] * (size_t)ch[0].args->resolution[1] * 3;
   if (img && !out) return fail(VR_ERR_ARGUMENT, "output is NULL");
   const size_t bytes = img * sizeof(float) * (size_t)n * (stereo ? 2 : 1);
@@ -1283,6 +1273,7 @@ int vr_render(vr_context *h, const vr_render_args *a, float *out) {
   if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   const size_t bytes = (size_t)a->resolution[0] * (size_t)a->resolution[1] * 3 * sizeof(float);
   if (bytes && !out) return fail(VR_ERR_ARGUMENT, "output is NULL");
   if (bytes > h->d_out_bytes) {
@@ -1306,6 +1297,7 @@ int vr_render_stereo(vr_context *h, const vr_render_args *a, float base, float *
   if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   const size_t bytes = (size_t)a->resolution[0] * (size_t)a->resolution[1] * 3 * sizeof(float);
   if (bytes && (!out_left || !out_right)) return fail(VR_ERR_ARGUMENT, "output is NULL");
   if (2 * bytes > h->d_out_bytes) {
@@ -1343,6 +1335,7 @@ int vr_render_device(vr_context *h, const vr_render_args *a, const vr_partition 
   if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   Frame F;
   return do_render(h, a, part, d_out, d_steps, (hipStream_t)stream, F);
   VR_GUARD_END
@@ -1370,6 +1363,7 @@ int vr_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *slab, 
   if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
+  vr_host::prune_retired();  // buffers whose last launch has completed
   Frame F;
   return do_render_slab(h, a, slab, part, d_state_in, d_state_out, (hipStream_t)stream, F);
   VR_GUARD_END

@@ -220,6 +220,52 @@ __global__ __launch_bounds__(256) void pad_volume_kernel(const float *__restrict
   }
 }
 
+// Padded planes [k0, k1) of the apron layout (vr_device.h) from source planes [z0, ...) held at src
+// (a chunk of the volume, or the whole of it), one padded row per workgroup iteration: a coalesced
+// read of the source row, a coalesced write of the padded row with its two border copies; the
+// statistics of the written values (nonfinite flag, max |x| -- border copies repeat interior
+// values, so they change neither) are folded in on the way (the upload path, vr_resources.h).
+__global__ __launch_bounds__(256) void pad_planes_kernel(const float *__restrict__ src, int64_t z0, int32_t nx,
+                                                         int32_t ny, int32_t nz, float *__restrict__ dst, int64_t k0,
+                                                         uint64_t rows, BufStats *st) {
+  const uint64_t px = (uint64_t)nx + 2, py = (uint64_t)ny + 2;
+  uint32_t bad = 0;
+  float mx = 0.f;
+  for (uint64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const uint64_t k = (uint64_t)k0 + row / py;
+    const int64_t j = (int64_t)(row % py);
+    const int64_t kk = (int64_t)k - 1, jj = j - 1;
+    const int64_t sk = (kk < 0 ? 0 : (kk > (int64_t)nz - 1 ? (int64_t)nz - 1 : kk)) - z0;
+    const int64_t sj = jj < 0 ? 0 : (jj > (int64_t)ny - 1 ? (int64_t)ny - 1 : jj);
+    const float *s = src + ((uint64_t)sk * (uint64_t)ny + (uint64_t)sj) * (uint64_t)nx;
+    float *d = dst + (k * py + (uint64_t)j) * px;
+    for (uint32_t i = threadIdx.x; i < px; i += blockDim.x) {
+      const uint32_t si = i == 0 ? 0u : (i > (uint32_t)nx ? (uint32_t)nx - 1 : i - 1);
+      const float v = s[si];
+      d[i] = v;
+      if (!(fabsf(v) <= 3.4028234e38f)) bad = 1;
+      else mx = fmaxf(mx, fabsf(v));
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    bad |= __shfl_xor(bad, off, 64);
+    mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+  }
+  __shared__ uint32_t sb[4];
+  __shared__ float sm[4];
+  if ((threadIdx.x & 63) == 0) {
+    sb[threadIdx.x >> 6] = bad;
+    sm[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t bb = sb[0] | sb[1] | sb[2] | sb[3];
+    const float m = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    if (bb) atomicOr(&st->nonfinite, 1u);
+    atomicMax(reinterpret_cast<unsigned int *>(&st->maxabs), __float_as_uint(m));  // m >= 0
+  }
+}
+
 // nonfinite flag and max |x| of a dense buffer (one atomic pair per workgroup)
 __global__ __launch_bounds__(256) void stats_kernel(const float *__restrict__ src, uint64_t n, BufStats *st) {
   uint32_t bad = 0;
@@ -440,6 +486,17 @@ hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int3
   uint64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(pad_volume_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, nx, ny, nz);
+  return hipGetLastError();
+}
+
+hipError_t launch_pad_planes(const float *src, int64_t z0, int32_t nx, int32_t ny, int32_t nz, float *dst, int64_t k0,
+                             int64_t k1, BufStats *st, hipStream_t s) {
+  const uint64_t rows = (uint64_t)(k1 - k0) * ((uint64_t)ny + 2);
+  if (!rows || nx <= 0 || ny <= 0 || nz <= 0) return hipSuccess;
+  // a few workgroups per CU that loop over rows: few dispatches, so an upload that runs beside a
+  // render (which holds most CU slots) is not held back by workgroup dispatch
+  const uint64_t blocks = rows < 2048 ? rows : 2048;
+  hipLaunchKernelGGL(pad_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, z0, nx, ny, nz, dst, k0, rows, st);
   return hipGetLastError();
 }
 

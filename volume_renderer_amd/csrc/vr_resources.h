@@ -1,0 +1,378 @@
+// vr_resources.h -- device-resource lifetime of libvrhip's host driver (included by vr_capi.hip only).
+//
+// The reference serialises everything on CUDA's legacy default stream: an upload or a texture
+// rebind can never overlap a render (volumeRender_kernel.cu:551-722 bind/copy synchronously, the
+// mex call returns after cudaDeviceSynchronize).  Here renders may be in flight on caller streams
+// (vr_render_device, vr_render_channels_device, vr_render_slab) while the host syncs the next frame's
+// volumes, so every launch records an event, and what a launch reads is kept until that event:
+//   - Event / record_event: a shared completion marker of one launch (or of an upload);
+//   - free_when_done: device memory released only after the last launch that read it (a buffer
+//     dropped while in flight is parked in the retired list, pruned at every API entry);
+//   - ConstRing: per-launch small constants (the light list) staged through a pinned host ring on
+//     the launch's own stream -- never a global buffer rewritten under a running kernel;
+//   - Uploader: the upload path: persistent per-device copy and pad streams
+//     and a device staging ring; a host volume crosses PCIe in plane chunks, each padded into the
+//     apron layout (and its statistics taken) on the device while the next chunks copy.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "vr_device.h"
+
+namespace vr {
+hipError_t launch_pad_planes(const float *src, int64_t z0, int32_t nx, int32_t ny, int32_t nz, float *dst, int64_t k0,
+                             int64_t k1, BufStats *st, hipStream_t s);
+}
+
+namespace vr_host {
+
+struct Event {
+  hipEvent_t e = nullptr;
+  ~Event() {
+    if (e) (void)hipEventDestroy(e);  // a pending event is released when it completes
+  }
+};
+using EventPtr = std::shared_ptr<Event>;
+
+inline hipError_t record_event(hipStream_t s, EventPtr &out) {
+  auto ev = std::make_shared<Event>();
+  hipError_t rc = hipEventCreateWithFlags(&ev->e, hipEventDisableTiming);
+  if (rc == hipSuccess) rc = hipEventRecord(ev->e, s);
+  if (rc == hipSuccess) out = ev;
+  return rc;
+}
+
+// completed (or never recorded); a query error counts as completed -- nothing better to wait for
+inline bool done(const EventPtr &ev) {
+  if (!ev || !ev->e) return true;
+  const hipError_t rc = hipEventQuery(ev->e);
+  if (rc == hipErrorNotReady) return false;
+  if (rc != hipSuccess) (void)hipGetLastError();
+  return true;
+}
+
+inline void wait(const EventPtr &ev) {
+  if (ev && ev->e) (void)hipEventSynchronize(ev->e);
+}
+
+struct Retired {
+  void *ptr;
+  int device;
+  EventPtr ev;
+  bool pinned;
+};
+
+inline std::vector<Retired> &retired() {
+  static std::vector<Retired> r;
+  return r;
+}
+
+inline void release(void *ptr, int device, bool pinned) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != device) (void)hipSetDevice(device);
+  if (pinned)
+    (void)hipHostFree(ptr);
+  else
+    (void)hipFree(ptr);
+  if (cur != device) (void)hipSetDevice(cur);
+}
+
+// free now if no launch still reads the allocation, else when `ev` completes
+inline void free_when_done(void *ptr, int device, const EventPtr &ev, bool pinned = false) {
+  if (!ptr) return;
+  if (done(ev))
+    release(ptr, device, pinned);
+  else
+    retired().push_back({ptr, device, ev, pinned});
+}
+
+// release what has completed; block = wait for everything first (before a retried allocation)
+inline void prune_retired(bool block = false) {
+  auto &r = retired();
+  size_t k = 0;
+  for (size_t i = 0; i < r.size(); ++i) {
+    if (block) wait(r[i].ev);
+    if (done(r[i].ev))
+      release(r[i].ptr, r[i].device, r[i].pinned);
+    else
+      r[k++] = r[i];
+  }
+  r.resize(k);
+}
+
+// Released volume buffers are kept for reuse by size (hipFree waits for the whole device, so
+// freeing the previous frame's buffer would stall the render in flight; a movie whose volume
+// changes every frame ping-pongs between two buffers).  Bounded: POOL_MAX bytes per device, the
+// oldest completed ones freed beyond that, everything on vr_delete or when an allocation fails.
+struct Pooled {
+  void *ptr;
+  int device;
+  size_t bytes;
+  EventPtr ev;
+};
+constexpr size_t POOL_MIN = 1ull << 20, POOL_MAX = 64ull << 30;
+
+inline std::vector<Pooled> &pool() {
+  static std::vector<Pooled> p;
+  return p;
+}
+
+inline size_t pool_bytes(int device) {
+  size_t t = 0;
+  for (const Pooled &q : pool())
+    if (q.device == device) t += q.bytes;
+  return t;
+}
+
+// release pooled buffers (all, or of one device: block = wait for their last launches first)
+inline void pool_clear(int device = -1) {
+  auto &p = pool();
+  size_t k = 0;
+  for (size_t i = 0; i < p.size(); ++i) {
+    if (device < 0 || p[i].device == device) {
+      wait(p[i].ev);
+      release(p[i].ptr, p[i].device, false);
+    } else {
+      p[k++] = p[i];
+    }
+  }
+  p.resize(k);
+}
+
+// hipMalloc that first reclaims pooled and retired buffers when the device is full
+inline hipError_t device_alloc(void **p, size_t bytes) {
+  hipError_t rc = hipMalloc(p, bytes);
+  if (rc == hipErrorOutOfMemory || rc == hipErrorMemoryAllocation) {
+    (void)hipGetLastError();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    pool_clear(dev);
+    prune_retired(true);
+    rc = hipMalloc(p, bytes);
+  }
+  return rc;
+}
+
+// a volume-sized allocation: a pooled buffer of exactly this size whose last launch completed, or
+// a new one
+inline hipError_t pooled_alloc(void **p, size_t bytes, int device) {
+  auto &q = pool();
+  for (size_t i = 0; i < q.size(); ++i) {
+    if (q[i].device == device && q[i].bytes == bytes && done(q[i].ev)) {
+      *p = q[i].ptr;
+      q.erase(q.begin() + (ptrdiff_t)i);
+      return hipSuccess;
+    }
+  }
+  return device_alloc(p, bytes);
+}
+
+// give a volume buffer back: pooled (it stays allocated) unless small or the pool is full
+inline void pooled_free(void *ptr, size_t bytes, int device, const EventPtr &ev) {
+  if (!ptr) return;
+  if (bytes < POOL_MIN || bytes > POOL_MAX) {
+    free_when_done(ptr, device, ev);
+    return;
+  }
+  auto &q = pool();
+  q.push_back({ptr, device, bytes, ev});
+  size_t total = pool_bytes(device);
+  for (size_t i = 0; i < q.size() && total > POOL_MAX;) {  // oldest completed first
+    if (q[i].device == device && done(q[i].ev) && q[i].ptr != ptr) {
+      total -= q[i].bytes;
+      release(q[i].ptr, device, false);
+      q.erase(q.begin() + (ptrdiff_t)i);
+    } else {
+      ++i;
+    }
+  }
+}
+
+// Per-launch constants through a pinned ring: slot i is rewritten only after the launch that last
+// read it completed (its event), so any number of in-flight launches on any streams each see their
+// own copy.  A payload larger than a slot gets a dedicated allocation freed after its launch.
+struct ConstRing {
+  static constexpr size_t SLOT = 4096;
+  static constexpr unsigned N = 256;
+  int device = -1;
+  char *host = nullptr, *dev = nullptr;
+  EventPtr ev[N];
+  unsigned next = 0;
+
+  hipError_t init(int d) {
+    if (host) return hipSuccess;
+    device = d;
+    hipError_t rc = hipHostMalloc(reinterpret_cast<void **>(&host), SLOT * N, hipHostMallocDefault);
+    if (rc == hipSuccess) rc = device_alloc(reinterpret_cast<void **>(&dev), SLOT * N);
+    return rc;
+  }
+};
+
+inline std::map<int, ConstRing> &rings() {
+  static std::map<int, ConstRing> r;
+  return r;
+}
+
+// What one launch reads: its buffers' owners are kept alive, and marked with the launch's event by
+// finish(); the staged constants' ring slot is released by the same event.
+template <class BufPtrT>
+struct LaunchRec {
+  hipStream_t stream = nullptr;
+  int device = 0;
+  std::vector<BufPtrT> reads;
+  int slot = -1;
+  void *big = nullptr;  // a dedicated constants allocation (payload > SLOT)
+
+  // a device copy of `bytes` of host data, ordered on the launch stream
+  hipError_t stage(const void *src, size_t bytes, const void **out) {
+    *out = nullptr;
+    if (!bytes) return hipSuccess;
+    if (bytes > ConstRing::SLOT) {
+      hipError_t rc = device_alloc(&big, bytes);
+      if (rc == hipSuccess) rc = hipMemcpy(big, src, bytes, hipMemcpyHostToDevice);
+      *out = big;
+      return rc;
+    }
+    ConstRing &R = rings()[device];
+    hipError_t rc = R.init(device);
+    if (rc != hipSuccess) return rc;
+    slot = (int)(R.next++ % ConstRing::N);
+    wait(R.ev[slot]);  // the launch that used this slot N launches ago
+    R.ev[slot].reset();
+    std::memcpy(R.host + (size_t)slot * ConstRing::SLOT, src, bytes);
+    rc = hipMemcpyAsync(R.dev + (size_t)slot * ConstRing::SLOT, R.host + (size_t)slot * ConstRing::SLOT, bytes,
+                        hipMemcpyHostToDevice, stream);
+    *out = R.dev + (size_t)slot * ConstRing::SLOT;
+    return rc;
+  }
+
+  // after the launch(es): everything read is released by their completion
+  hipError_t finish() {
+    EventPtr ev;
+    hipError_t rc = record_event(stream, ev);
+    if (rc != hipSuccess) {  // cannot track: fall back to waiting here
+      (void)hipGetLastError();
+      rc = hipStreamSynchronize(stream);
+    }
+    for (auto &b : reads)
+      if (b) b->last_use = ev;
+    if (slot >= 0) rings()[device].ev[slot] = ev;
+    if (big) free_when_done(big, device, ev);
+    big = nullptr;
+    return rc;
+  }
+};
+
+// The upload path of one device (replaces the per-sync cudaMalloc3DArray +
+// cudaMemcpy3D of volumeRender_kernel.cu:659-672).  Host volumes cross PCIe in plane chunks of up
+// to CHUNK bytes on a copy stream into a ring of NS device staging slots; each chunk is padded into
+// the destination (apron layout, vr_device.h, statistics folded in) on a separate, highest-priority
+// pad stream as soon as it has landed, while the copy stream moves on to the next slot (it waits
+// only for the pad of the chunk that last used that slot).  So when a render of the previous frame
+// holds the CUs and the pads run slowly beside it, the PCIe copies still stream back to back.
+// Device volumes are padded straight from the caller's buffer.  The call returns when the volume
+// is resident (the caller's pointer is borrowed for the call only, render.cpp:307-342) -- renders
+// already in flight on other streams keep running meanwhile.
+struct Uploader {
+  static constexpr size_t CHUNK = 1ull << 30, WHOLE = 8ull << 30;
+  static constexpr int NS = 4;
+  int device = -1;
+  hipStream_t stream = nullptr;      // copies
+  hipStream_t pad_stream = nullptr;  // pads + statistics
+  hipEvent_t copied[NS] = {}, padded[NS] = {};
+  float *staging = nullptr;  // nslots slots of slot_floats
+  size_t slot_floats = 0, nslots = 0;
+  vr::BufStats *d_stats = nullptr, *h_stats = nullptr;
+
+  hipError_t init(int d) {
+    if (stream) return hipSuccess;
+    device = d;
+    int lo = 0, hi = 0;
+    hipError_t rc = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (rc == hipSuccess) rc = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+    if (rc == hipSuccess) rc = hipStreamCreateWithPriority(&pad_stream, hipStreamNonBlocking, hi);
+    for (int i = 0; i < NS && rc == hipSuccess; ++i) {
+      rc = hipEventCreateWithFlags(&copied[i], hipEventDisableTiming);
+      if (rc == hipSuccess) rc = hipEventCreateWithFlags(&padded[i], hipEventDisableTiming);
+    }
+    if (rc == hipSuccess) rc = device_alloc(reinterpret_cast<void **>(&d_stats), sizeof(vr::BufStats));
+    if (rc == hipSuccess) rc = hipHostMalloc(reinterpret_cast<void **>(&h_stats), sizeof(vr::BufStats), hipHostMallocDefault);
+    return rc;
+  }
+
+  hipError_t ensure_staging(size_t floats) {
+    if (floats <= slot_floats) return hipSuccess;
+    nslots = 0;
+    if (staging) (void)hipFree(staging);  // both upload streams are idle between uploads
+    staging = nullptr;
+    slot_floats = 0;
+    const size_t slots = floats * sizeof(float) >= WHOLE / 2 ? 1 : NS;  // whole-volume staging: one slot
+    hipError_t rc = device_alloc(reinterpret_cast<void **>(&staging), slots * floats * sizeof(float));
+    if (rc == hipSuccess) {
+      slot_floats = floats;
+      nslots = slots;
+    }
+    return rc;
+  }
+
+  // src (host or device, per `on_device`) -> dst (padded, (nx+2)(ny+2)(nz+2) floats); *st = stats
+  hipError_t upload(const float *src, bool on_device, int32_t nx, int32_t ny, int32_t nz, float *dst,
+                    vr::BufStats *st) {
+    hipError_t rc = hipMemsetAsync(d_stats, 0, sizeof(vr::BufStats), pad_stream);
+    const uint64_t plane = (uint64_t)nx * (uint64_t)ny;
+    if (rc == hipSuccess && on_device) {
+      // device data is read after the work already queued on the null stream (which orders after
+      // every blocking stream) -- as the previous null-stream upload was -- e.g. a torch tensor
+      // just written on torch's default stream
+      EventPtr ev;
+      rc = record_event(nullptr, ev);
+      if (rc == hipSuccess) rc = hipStreamWaitEvent(pad_stream, ev->e, 0);
+      if (rc == hipSuccess) rc = vr::launch_pad_planes(src, 0, nx, ny, nz, dst, 0, (int64_t)nz + 2, d_stats, pad_stream);
+    } else if (rc == hipSuccess) {
+      // up to WHOLE bytes the volume crosses in one copy and is padded once it has landed: a pad
+      // that runs beside a render in flight (the previous frame's) is slow, and between chunks it
+      // would hold up the copies (measured: 1024^3 movie 98 ms per frame chunked vs 82 whole)
+      const uint64_t bytes = plane * (uint64_t)nz * sizeof(float);
+      uint64_t chunk = bytes <= WHOLE ? bytes : CHUNK;
+      if (const char *ev = std::getenv("VR_UPLOAD_CHUNK_MB")) chunk = std::max<uint64_t>(1, std::strtoull(ev, nullptr, 10)) << 20;
+      const uint64_t per = std::max<uint64_t>(1, chunk / (plane * sizeof(float)));
+      const uint64_t chunk_planes = std::min<uint64_t>(per, (uint64_t)nz);
+      rc = ensure_staging(chunk_planes * plane);
+      for (uint64_t z0 = 0, c = 0; rc == hipSuccess && z0 < (uint64_t)nz; z0 += chunk_planes, ++c) {
+        const uint64_t z1 = std::min<uint64_t>((uint64_t)nz, z0 + chunk_planes);
+        const int k = (int)(c % nslots);
+        float *slot = staging + (size_t)k * slot_floats;
+        if (c >= nslots) rc = hipStreamWaitEvent(stream, padded[k], 0);  // the slot's previous chunk is padded
+        if (rc == hipSuccess)
+          rc = hipMemcpyAsync(slot, src + z0 * plane, (z1 - z0) * plane * sizeof(float), hipMemcpyHostToDevice, stream);
+        if (rc == hipSuccess) rc = hipEventRecord(copied[k], stream);
+        if (rc == hipSuccess) rc = hipStreamWaitEvent(pad_stream, copied[k], 0);
+        // padded planes: source plane z sits at z + 1; the apron planes 0 and nz + 1 replicate the ends
+        const int64_t k0 = z0 == 0 ? 0 : (int64_t)z0 + 1;
+        const int64_t k1 = z1 == (uint64_t)nz ? (int64_t)nz + 2 : (int64_t)z1 + 1;
+        if (rc == hipSuccess) rc = vr::launch_pad_planes(slot, (int64_t)z0, nx, ny, nz, dst, k0, k1, d_stats, pad_stream);
+        if (rc == hipSuccess) rc = hipEventRecord(padded[k], pad_stream);
+      }
+    }
+    if (rc == hipSuccess) rc = hipMemcpyAsync(h_stats, d_stats, sizeof(vr::BufStats), hipMemcpyDeviceToHost, pad_stream);
+    if (rc == hipSuccess) rc = hipStreamSynchronize(pad_stream);  // the last pad followed the last copy
+    if (rc == hipSuccess) rc = hipStreamSynchronize(stream);
+    if (rc == hipSuccess) *st = *h_stats;
+    return rc;
+  }
+};
+
+inline std::map<int, Uploader> &uploaders() {
+  static std::map<int, Uploader> u;
+  return u;
+}
+
+}  // namespace vr_host
