@@ -104,7 +104,10 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   const f3 ps = mk((pos.x - bmin.x) * bsc.x, (pos.y - bmin.y) * bsc.y, (pos.z - bmin.z) * bsc.z);
   // unclamped axes (axis_raw): exact on the LDS path, clamped by fetch_at on the global one.
   // The fast variant's half-texel gradient taps need the raw fraction's half split as well.
+  // MODE 1 with SHARE2: the launch is known to take the half-texel taps (P.tap_half; the exact
+  // tap code is not compiled in, which frees registers); without it P.tap_half decides per sample.
   constexpr bool HALF_TAPS = VR_MARCH_FAST && MODE == 1;
+  constexpr bool HALF_ONLY = HALF_TAPS && SHARE2;
   AxS sx{}, sy{}, sz{};
   Ax ax, ay, az;
   if constexpr (HALF_TAPS) {
@@ -124,7 +127,14 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
   const int ayz = lz * B.pxy + ly * B.px;  // slot word of (0, ly, lz)
   const int ac = ayz + lx;
-  const float em_s = fetch_at<BIG>(E, L, B, staged && inx && iny && inz, ac, ax, ay, az);
+  Cell C;  // the centre's partial sums, for the half-texel taps (valid where the centre is staged)
+  float em_s;
+  if constexpr (HALF_TAPS) {
+    if (staged && inx && iny && inz) em_s = lds_tri_cell(L, B, ac, ax.w, ay.w, az.w, C);
+    else em_s = fetch<BIG>(E, clamp_ax(ax, E.nx), clamp_ax(ay, E.ny), clamp_ax(az, E.nz));
+  } else {
+    em_s = fetch_at<BIG>(E, L, B, staged && inx && iny && inz, ac, ax, ay, az);
+  }
   const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
   const float e = P.fe * em_s;
   const float a = P.fa * ab_s;
@@ -137,7 +147,15 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     f3 g;
     if (MODE == 1 && (VR_ABLATE & 4)) {
       g = mk(ps.x, ps.y, em_s);
-    } else if (HALF_TAPS && P.tap_half) {
+    } else if (HALF_TAPS && (HALF_ONLY || P.tap_half) &&
+               __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
+                     (unsigned)(ly + (sy.hi ? 1 : 0) - 1) < (unsigned)(B.ey - 2) &&
+                     (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2))) {
+      // every shading lane's taps lie in the staged box (the tap cells a - 1 .. a + 1 per axis,
+      // a = i + hi): the taps from the slot with their shared voxels and partial sums
+      const f3 d = half_grad_lds(L, B, ac, sx, sy, sz, ax.w, ay.w, az.w, C);
+      g = mk(d.x * 0.5f, d.y * 0.5f, d.z * 0.5f);
+    } else if (HALF_TAPS && (HALF_ONLY || P.tap_half)) {
       // fast variant, gradient offset of exactly half a texel on every axis (a power-of-two cube,
       // vr_capi.hip half_texel_taps): each axis' two taps derived from the centre's (half_taps);
       // in the slot the plus tap's cell is the centre's, or the next one along the axis, and the
@@ -183,7 +201,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
       g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
             fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
       g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
-    } else if (SHARE2) {
+    } else if (MODE == 2 && SHARE2) {
       const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
       if (P.gvec)
         g = fetch_vec<BIG>(P.gvec, P.gx, cx, cy, cz);
@@ -772,7 +790,10 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
     return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {
     case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);
-    case 1: return ab_alias ? launch_m<1, true, false>(P, grid, s, big) : launch_m<1, false, false>(P, grid, s, big);
+    case 1:  // SH: the half-texel tap launch (fast variant only; see sample_at)
+      if (VR_MARCH_FAST && P.tap_half)
+        return ab_alias ? launch_m<1, true, true>(P, grid, s, big) : launch_m<1, false, true>(P, grid, s, big);
+      return ab_alias ? launch_m<1, true, false>(P, grid, s, big) : launch_m<1, false, false>(P, grid, s, big);
     default:
       if (share) return ab_alias ? launch_m<2, true, true>(P, grid, s, big) : launch_m<2, false, true>(P, grid, s, big);
       return ab_alias ? launch_m<2, true, false>(P, grid, s, big) : launch_m<2, false, false>(P, grid, s, big);

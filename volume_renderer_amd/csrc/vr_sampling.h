@@ -382,6 +382,32 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     const float alpha_n = acospi_q(dot3(n, li) * (rn * __builtin_amdgcn_rsqf(dot3(li, li))));
     const AxF la = axis_lut(alpha_n, P.lut.fnx);
     int i = 0;
+    if (P.lut.p != nullptr && P.lut.small && !P.lut.one) {
+      // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
+      // lights, so that a pair's eight LUT row loads issue together, ahead of their lerps
+      for (; i + 1 < P.num_lights; i += 2) {
+        const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+        const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
+        const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
+        const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
+        const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
+        const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
+        const float beta0 = acospi_q(dlo0 * (rn * __builtin_amdgcn_rsqf(dot3(lo0, lo0))));
+        const float gamma0 = acospi_q(dot3(lip, lop0) * (rlip * __builtin_amdgcn_rsqf(dot3(lop0, lop0))));
+        const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
+        const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
+        const float light0 = fetch_small(P.lut, la, axis_lut(beta0, P.lut.fny), axis_lut(gamma0, P.lut.fnz));
+        const float light1 = fetch_small(P.lut, la, axis_lut(beta1, P.lut.fny), axis_lut(gamma1, P.lut.fnz));
+        const float rl0 = refl * light0;
+        ir = fmaf(rl0 * L0.cr, P.color[0], ir);
+        ig = fmaf(rl0 * L0.cg, P.color[1], ig);
+        ib = fmaf(rl0 * L0.cb, P.color[2], ib);
+        const float rl1 = refl * light1;
+        ir = fmaf(rl1 * L1.cr, P.color[0], ir);
+        ig = fmaf(rl1 * L1.cg, P.color[1], ig);
+        ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+      }
+    }
     for (; i + 1 < P.num_lights; i += 2) {
       const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
       const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);

@@ -73,6 +73,70 @@ __device__ __forceinline__ float lds_tri(const float *L, const Box &B, int a, fl
   return lerp(c0, c1, wz);
 }
 
+// The partial sums of one staged trilinear fetch (lds_tri's c00 .. c1), kept by the centre sample
+// for the gradient taps that share them (half_grad_lds).
+struct Cell {
+  float c00, c10, c01, c11, c0, c1;
+};
+__device__ __forceinline__ float lds_tri_cell(const float *L, const Box &B, int a, float wx, float wy, float wz,
+                                              Cell &C) {
+  C.c00 = lerp(L[a], L[a + 1], wx);
+  C.c10 = lerp(L[a + B.px], L[a + B.px + 1], wx);
+  C.c01 = lerp(L[a + B.pxy], L[a + B.pxy + 1], wx);
+  C.c11 = lerp(L[a + B.pxy + B.px], L[a + B.pxy + B.px + 1], wx);
+  C.c0 = lerp(C.c00, C.c10, wy);
+  C.c1 = lerp(C.c01, C.c11, wy);
+  return lerp(C.c0, C.c1, wz);
+}
+
+// The six half-texel gradient taps of the fast variant (vr_sampling.h half_taps) from the slot, for
+// a sample whose centre cell (slot word ac, partial sums C, weights wx wy wz) and tap cells all lie
+// in the staged box.  Each tap is the trilinear fetch fetch_at would take -- same voxels, same
+// weights, the same lerps in the same order (x, then y, then z) -- but what two taps or a tap and
+// the centre compute alike is computed once: the x taps read their three voxels per row (the minus
+// and plus cells share the middle one); the y taps' x-interpolated rows are the centre's c00 .. c11
+// except one extra row pair; the z taps' xy-interpolated planes are the centre's c0, c1 except one
+// extra plane.  20 voxels and 27 lerps instead of 48 voxels and 42 lerps, with no per-tap box
+// test.  Returns the unhalved differences (plus - minus) per axis.
+__device__ __forceinline__ f3 half_grad_lds(const float *L, const Box &B, int ac, const AxS &sx, const AxS &sy,
+                                            const AxS &sz, float wx, float wy, float wz, const Cell &C) {
+  f3 g;
+  {  // x: cells a - 1 (minus) and a (plus), a = i + hi; three voxels per (y, z) row from a - 1
+    const float tx = sx.w + (sx.hi ? -0.5f : 0.5f);
+    const int w = ac + (sx.hi ? 0 : -1);
+    float m[4], p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = w + ((r & 1) ? B.px : 0) + ((r & 2) ? B.pxy : 0);
+      const float x0 = L[o], x1 = L[o + 1], x2 = L[o + 2];
+      m[r] = lerp(x0, x1, tx);
+      p[r] = lerp(x1, x2, tx);
+    }
+    const float gm = lerp(lerp(m[0], m[1], wy), lerp(m[2], m[3], wy), wz);
+    const float gp = lerp(lerp(p[0], p[1], wy), lerp(p[2], p[3], wy), wz);
+    g.x = gp - gm;
+  }
+  {  // y: rows b - 1, b, b + 1 (b = j + hi) of the x-interpolated values; one row pair is new
+    const float ty = sy.w + (sy.hi ? -0.5f : 0.5f);
+    const int w = ac + (sy.hi ? 2 * B.px : -B.px);
+    const float e0 = lerp(L[w], L[w + 1], wx), e1 = lerp(L[w + B.pxy], L[w + B.pxy + 1], wx);
+    const float y00 = sy.hi ? C.c00 : e0, y01 = sy.hi ? C.c10 : C.c00, y02 = sy.hi ? e0 : C.c10;  // z
+    const float y10 = sy.hi ? C.c01 : e1, y11 = sy.hi ? C.c11 : C.c01, y12 = sy.hi ? e1 : C.c11;  // z + 1
+    const float gm = lerp(lerp(y00, y01, ty), lerp(y10, y11, ty), wz);
+    const float gp = lerp(lerp(y01, y02, ty), lerp(y11, y12, ty), wz);
+    g.y = gp - gm;
+  }
+  {  // z: planes c - 1, c, c + 1 (c = k + hi) of the xy-interpolated values; one plane is new
+    const float tz = sz.w + (sz.hi ? -0.5f : 0.5f);
+    const int w = ac + (sz.hi ? 2 * B.pxy : -B.pxy);
+    const float q0 = lerp(L[w], L[w + 1], wx), q1 = lerp(L[w + B.px], L[w + B.px + 1], wx);
+    const float pe = lerp(q0, q1, wy);
+    const float z0 = sz.hi ? C.c0 : pe, z1 = sz.hi ? C.c1 : C.c0, z2 = sz.hi ? pe : C.c1;
+    g.z = lerp(z1, z2, tz) - lerp(z0, z1, tz);
+  }
+  return g;
+}
+
 // Slot coordinates of a tap pair base and whether the cell [l, l+1] lies in the box along it.
 __device__ __forceinline__ int slot_coord(int i, int r) { return (int)((uint32_t)i + 1u - (uint32_t)r); }
 __device__ __forceinline__ bool in_box(int l, int e) {
