@@ -228,6 +228,29 @@ int vr_synth_shell_planes_device(float *d_out, uint64_t n, uint64_t z_first, uin
 int vr_gradient_device(const float *d_data, const uint64_t dims[3], float *d_gx, float *d_gy, float *d_gz,
                        void *stream);
 
+/* --- the MATLAB-side volume preprocessing on the device ----------------- */
+
+/* HenyeyGreenstein(N, g) (HenyeyGreenstein.cc:29-96) into device memory d_out[N*N*N], same layout as
+ * vr_henyey_greenstein.  The sines / cosines are the host generator's; the power of 3 comes from the
+ * device math library, so elements can differ from the host LUT in the last bits (measured at
+ * most 3 ulp, ~91 % bit-identical; tests/test_volume_ops.py bounds it at 4 ulp).  Returns when the LUT is written. */
+int vr_henyey_greenstein_device(uint32_t n, float g, float *d_out, void *stream);
+
+/* Volume.normalize(newMin, newMax) (Volume.m:208-220) of n single values on the device:
+ * (x - min) * single(newMax - newMin) / (max - min) + single(newMin) in MATLAB's single arithmetic,
+ * min / max omitting NaN.  d_out may equal d_in.  Asynchronous on `stream`. */
+int vr_normalize_device(const float *d_in, uint64_t n, double new_min, double new_max, float *d_out, void *stream);
+
+/* Volume.resize(newsize) (Volume.m:93-106: imresize3, or imresize for 2-D data) of a column-major
+ * (d0, d1, d2) single volume on the device into d_out[out0*out1*out2]: MATLAB's default cubic
+ * kernel, antialiasing when shrinking, mirrored ends, separable passes (double accumulation, single
+ * result) along the axes in order of increasing scale.  Returns when done. */
+int vr_resize_device(const float *d_in, const uint64_t in_dims[3], const uint64_t out_dims[3], float *d_out,
+                     void *stream);
+
+/* The weights / 0-based indices of one resize axis (out_len x *P, row-major), for tests. */
+int vr_resize_contributions(uint64_t in_len, uint64_t out_len, int32_t *P, double *w, int32_t *idx);
+
 /* Host-side reproduction of the upload/slot state machine (syncWithDevice,
  * volumeRender_kernel.cu:739-867) for unit tests: returns the slot indices after a sync with the
  * given similarity/update flags starting from `idx` (emission, absorption, reflection). */

@@ -407,3 +407,78 @@ def rotation(alpha=0.0, beta=0.0, gamma=0.0, R=None) -> np.ndarray:
     Ry = np.array([[cd(beta), 0, sd(beta)], [0, 1, 0], [-sd(beta), 0, cd(beta)]])
     Rz = np.array([[cd(gamma), -sd(gamma), 0], [sd(gamma), cd(gamma), 0], [0, 0, 1]])
     return R @ Rx @ Ry @ Rz
+
+
+# ---------------------------------------------------------------------------------------------
+# MATLAB-side volume preprocessing, restated for the device versions' tests.
+# Parity unpinned: no MATLAB here; these follow the published imresize / imresize3 algorithm
+# (contributions(): cubic kernel, antialiasing when shrinking, mirrored ends) and Volume.m.
+
+def _cubic(x):
+    """imresize's cubic kernel (a = -0.5), double."""
+    ax = np.abs(x)
+    ax2 = ax * ax
+    ax3 = ax * ax * ax
+    return ((1.5 * ax3 - 2.5 * ax2 + 1.0) * (ax <= 1.0) +
+            (-0.5 * ax3 + 2.5 * ax2 - 4.0 * ax + 2.0) * ((1.0 < ax) & (ax <= 2.0)))
+
+
+def resize_contributions(in_len: int, out_len: int):
+    """imresize contributions() for one axis (Volume.m:93-106 -> imresize3): weights [out, P]
+    (double, row-normalised) and 0-based source indices [out, P] (mirrored at the ends), columns
+    zero for every output dropped."""
+    scale = out_len / in_len
+    aa = scale < 1.0
+    width = 4.0 / scale if aa else 4.0
+    x = np.arange(1, out_len + 1, dtype=np.float64)[:, None]
+    u = x / scale + 0.5 * (1.0 - 1.0 / scale)
+    left = np.floor(u - width / 2.0)
+    P = int(np.ceil(width)) + 2
+    ind = left + np.arange(P, dtype=np.float64)[None, :]
+    d = u - ind
+    w = scale * _cubic(scale * d) if aa else _cubic(d)
+    s = np.zeros((out_len, 1))
+    for p in range(P):  # row sums in tap order
+        s[:, 0] = s[:, 0] + w[:, p]
+    w = w / s
+    n = in_len
+    k = np.mod(ind.astype(np.int64) - 1, 2 * n)
+    idx = np.where(k < n, k, 2 * n - 1 - k)
+    keep = np.any(w != 0.0, axis=0)
+    return w[:, keep], idx[:, keep].astype(np.int32)
+
+
+def resize(data: np.ndarray, newsize) -> np.ndarray:
+    """Volume.resize: separable passes along the axes in order of increasing scale (stable), each
+    out = sum_p w * in[idx] accumulated in double in tap order and rounded to single; axes whose
+    length does not change are skipped."""
+    a = np.asarray(data, np.float32)
+    new = tuple(int(v) for v in np.asarray(newsize).reshape(-1))
+    shp = a.shape + (1,) * (3 - a.ndim)
+    out_shape = new + (1,) * (3 - len(new))
+    a = a.reshape(shp, order="F")
+    scales = [out_shape[i] / shp[i] for i in range(3)]
+    order = sorted(range(3), key=lambda i: scales[i])
+    for dim in order:
+        if out_shape[dim] == a.shape[dim]:
+            continue
+        w, idx = resize_contributions(a.shape[dim], out_shape[dim])
+        src = np.moveaxis(a, dim, 0).astype(np.float64)
+        acc = np.zeros((out_shape[dim],) + src.shape[1:], np.float64)
+        for p in range(w.shape[1]):
+            acc = acc + w[:, p].reshape((-1,) + (1,) * (src.ndim - 1)) * src[idx[:, p]]
+        a = np.moveaxis(acc.astype(np.float32), 0, dim)
+    return np.asfortranarray(a.reshape(new if len(new) == np.asarray(data).ndim else out_shape, order="F"))
+
+
+def normalize(data: np.ndarray, new_min: float, new_max: float) -> np.ndarray:
+    """Volume.normalize (Volume.m:208-220) in single: max / min omit NaN; each operation rounded."""
+    d = np.asarray(data, np.float32)
+    valid = d[d == d]
+    mx = valid.max() if valid.size else np.float32(np.nan)
+    mn = valid.min() if valid.size else np.float32(np.nan)
+    with np.errstate(all="ignore"):
+        t1 = d - mn
+        t2 = t1 * np.float32(float(new_max) - float(new_min))
+        t3 = t2 / np.float32(mx - mn)
+        return t3 + np.float32(new_min)

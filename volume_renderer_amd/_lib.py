@@ -88,6 +88,10 @@ SIGNATURES = [
     ("vr_synth_shell_device", c_int, [c_void_p, c_uint64, c_void_p]),
     ("vr_synth_shell_planes_device", c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
     ("vr_gradient_device", c_int, [c_void_p, POINTER(c_uint64), c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("vr_henyey_greenstein_device", c_int, [c_uint32, c_float, c_void_p, c_void_p]),
+    ("vr_normalize_device", c_int, [c_void_p, c_uint64, ctypes.c_double, ctypes.c_double, c_void_p, c_void_p]),
+    ("vr_resize_device", c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_void_p, c_void_p]),
+    ("vr_resize_contributions", c_int, [c_uint64, c_uint64, POINTER(c_int32), c_void_p, c_void_p]),
     ("vr_debug_slot_transition", c_int, [POINTER(c_int32), c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                          POINTER(c_int32), POINTER(c_int32)]),
     ("vr_last_error", c_char_p, []),

@@ -64,6 +64,12 @@ hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc,
                            int64_t max_cols, float *out, hipStream_t s);
 hipError_t launch_synth_shell(float *out, uint64_t n, uint64_t z_first, uint64_t nz, hipStream_t s);
 hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, float *gy, float *gz, hipStream_t s);
+hipError_t launch_hg_lut(uint32_t n, const float *sn, const float *cs, float g, float g2, float num, float *out,
+                         hipStream_t s);
+hipError_t launch_normalize(const float *d, uint64_t n, uint32_t *mm, float range, float new_min, float *out,
+                            hipStream_t s);
+hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, uint64_t out_len, const double *w,
+                             const int32_t *idx, int32_t P, float *out, hipStream_t s);
 }  // namespace vr
 
 #ifndef VR_DEPTH_ROUNDS_K1
@@ -952,6 +958,65 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
 
 double mb(uint64_t b) { return (double)b / (1024.0 * 1024.0); }
 
+// imresize's contributions along one axis (Volume.resize -> imresize3, Volume.m:93-106; MATLAB's
+// default: cubic kernel of width 4, antialiasing when shrinking): per output index o (1-based x),
+// u = x/scale + (1 - 1/scale)/2, the P = ceil(width) + 2 taps from floor(u - width/2), weights
+// h(u - index) normalised by their row sum, indices mirrored at the ends ([1..n, n..1]), columns
+// that are zero for every output removed.  Double precision throughout; 0-based indices out.
+double cubic(double x) {
+  const double ax = std::fabs(x), ax2 = ax * ax, ax3 = ax * ax * ax;
+  return (1.5 * ax3 - 2.5 * ax2 + 1.0) * (ax <= 1.0 ? 1.0 : 0.0) +
+         (-0.5 * ax3 + 2.5 * ax2 - 4.0 * ax + 2.0) * ((1.0 < ax && ax <= 2.0) ? 1.0 : 0.0);
+}
+void resize_contributions(uint64_t in_len, uint64_t out_len, std::vector<double> &w, std::vector<int32_t> &idx,
+                          int32_t &P) {
+  const double scale = (double)out_len / (double)in_len;
+  const bool aa = scale < 1.0;
+  const double width = aa ? 4.0 / scale : 4.0;
+  const int32_t P0 = (int32_t)std::ceil(width) + 2;
+  std::vector<double> w0((size_t)out_len * P0);
+  std::vector<int64_t> i0((size_t)out_len * P0);
+  for (uint64_t o = 0; o < out_len; ++o) {
+    const double x = (double)(o + 1);
+    const double u = x / scale + 0.5 * (1.0 - 1.0 / scale);
+    const double left = std::floor(u - width / 2.0);
+    double sum = 0.0;
+    for (int32_t p = 0; p < P0; ++p) {
+      const double ind = left + p;
+      const double d = u - ind;
+      const double h = aa ? scale * cubic(scale * d) : cubic(d);
+      w0[o * P0 + p] = h;
+      i0[o * P0 + p] = (int64_t)ind;
+      sum = sum + h;
+    }
+    for (int32_t p = 0; p < P0; ++p) w0[o * P0 + p] = w0[o * P0 + p] / sum;
+  }
+  // mirror: aux = [1:n, n:-1:1], index -> aux(mod(index - 1, 2n) + 1)
+  const int64_t n = (int64_t)in_len, m = 2 * n;
+  for (auto &i : i0) {
+    int64_t k = (i - 1) % m;
+    if (k < 0) k += m;
+    i = k < n ? k : (m - 1 - k);  // 0-based
+  }
+  std::vector<char> keep(P0, 0);
+  for (uint64_t o = 0; o < out_len; ++o)
+    for (int32_t p = 0; p < P0; ++p)
+      if (w0[o * P0 + p] != 0.0) keep[p] = 1;
+  P = 0;
+  for (int32_t p = 0; p < P0; ++p) P += keep[p];
+  w.assign((size_t)out_len * P, 0.0);
+  idx.assign((size_t)out_len * P, 0);
+  for (uint64_t o = 0; o < out_len; ++o) {
+    int32_t q = 0;
+    for (int32_t p = 0; p < P0; ++p) {
+      if (!keep[p]) continue;
+      w[o * P + q] = w0[o * P0 + p];
+      idx[o * P + q] = (int32_t)i0[o * P0 + p];
+      ++q;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1437,6 +1502,120 @@ int vr_debug_slot_transition(const int32_t idx_in[3], int32_t sim_em_ab, int32_t
 }
 
 #define HG_PI ((float)3.141592653589793238462643383279502884197169399375105820)
+
+// HenyeyGreenstein on the device: the generator's expression per element on
+// the GPU, with the sines / cosines of k*pi/N computed here exactly as the host generator does.
+int vr_henyey_greenstein_device(uint32_t n, float g, float *d_out, void *stream) {
+  if (g > 1 || g < -1) return fail(VR_ERR_ARGUMENT, "g must be in interval [-1,1]");
+  if (n && !d_out) return fail(VR_ERR_ARGUMENT, "output is NULL");
+  if (!n) return VR_OK;
+  VR_GUARD_BEGIN
+  const float frac_half = HG_PI / n;
+  std::vector<float> tab(2 * (size_t)n);
+  for (uint32_t k = 0; k < n; ++k) {
+    const float ang = k * frac_half;
+    tab[k] = sinf(ang);
+    tab[n + k] = cosf(ang);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  float *d_tab = nullptr;
+  VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_tab), tab.size() * sizeof(float), s));
+  VR_HIP(hipMemcpyAsync(d_tab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  VR_HIP(vr::launch_hg_lut(n, d_tab, d_tab + n, g, powf(g, 2.f), 1.f - powf(g, 2.f), d_out, s));
+  VR_HIP(hipFreeAsync(d_tab, s));
+  VR_HIP(hipStreamSynchronize(s));  // the host table is borrowed by the copy
+  return VR_OK;
+  VR_GUARD_END
+}
+
+// Volume.normalize(newMin, newMax) on the device (Volume.m:208-220), d_out may equal d_in.
+int vr_normalize_device(const float *d_in, uint64_t n, double new_min, double new_max, float *d_out, void *stream) {
+  if (n && (!d_in || !d_out)) return fail(VR_ERR_ARGUMENT, "NULL buffer");
+  if (!n) return VR_OK;
+  VR_GUARD_BEGIN
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t *mm = nullptr;
+  VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&mm), 2 * sizeof(uint32_t), s));
+  // MATLAB: (newMax - newMin) in double, then single with the single data; newMin single likewise
+  VR_HIP(vr::launch_normalize(d_in, n, mm, (float)(new_max - new_min), (float)new_min, d_out, s));
+  VR_HIP(hipFreeAsync(mm, s));
+  return VR_OK;
+  VR_GUARD_END
+}
+
+// Volume.resize(newsize) on the device (Volume.m:93-106 -> imresize3 / imresize): separable cubic
+// passes with antialiasing when shrinking, the axes in order of increasing scale (stable), an axis
+// whose length does not change skipped (its contributions are the identity).
+int vr_resize_device(const float *d_in, const uint64_t in_dims[3], const uint64_t out_dims[3], float *d_out,
+                     void *stream) {
+  if (!in_dims || !out_dims) return fail(VR_ERR_ARGUMENT, "dims is NULL");
+  uint64_t nin = 1, nout = 1;
+  for (int i = 0; i < 3; ++i) {
+    if (in_dims[i] > 0x7FFFFFFFull || out_dims[i] > 0x7FFFFFFFull) return fail(VR_ERR_UNSUPPORTED, "dimension too large");
+    nin *= in_dims[i];
+    nout *= out_dims[i];
+  }
+  if (!nout) return VR_OK;
+  if (!nin) return fail(VR_ERR_ARGUMENT, "cannot resize an empty volume");
+  if (!d_in || !d_out) return fail(VR_ERR_ARGUMENT, "NULL buffer");
+  VR_GUARD_BEGIN
+  hipStream_t s = (hipStream_t)stream;
+  int order[3] = {0, 1, 2};
+  double sc[3];
+  for (int i = 0; i < 3; ++i) sc[i] = (double)out_dims[i] / (double)in_dims[i];
+  std::stable_sort(order, order + 3, [&](int a, int b) { return sc[a] < sc[b]; });
+  std::vector<int> passes;
+  for (int k = 0; k < 3; ++k)
+    if (out_dims[order[k]] != in_dims[order[k]]) passes.push_back(order[k]);
+  if (passes.empty()) {
+    VR_HIP(hipMemcpyAsync(d_out, d_in, nin * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return VR_OK;
+  }
+  uint64_t cur[3] = {in_dims[0], in_dims[1], in_dims[2]};
+  const float *src = d_in;
+  std::vector<void *> temps;
+  for (size_t k = 0; k < passes.size(); ++k) {
+    const int dim = passes[k];
+    std::vector<double> w;
+    std::vector<int32_t> idx;
+    int32_t P = 0;
+    resize_contributions(cur[dim], out_dims[dim], w, idx, P);
+    double *d_w = nullptr;
+    int32_t *d_idx = nullptr;
+    VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_w), w.size() * sizeof(double), s));
+    VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_idx), idx.size() * sizeof(int32_t), s));
+    temps.push_back(d_w);
+    temps.push_back(d_idx);
+    VR_HIP(hipMemcpyAsync(d_w, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    VR_HIP(hipMemcpyAsync(d_idx, idx.data(), idx.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    uint64_t nxt[3] = {cur[0], cur[1], cur[2]};
+    nxt[dim] = out_dims[dim];
+    float *dst = d_out;
+    if (k + 1 < passes.size()) {
+      VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&dst), nxt[0] * nxt[1] * nxt[2] * sizeof(float), s));
+      temps.push_back(dst);
+    }
+    VR_HIP(vr::launch_resize_dim(src, cur, dim, out_dims[dim], d_w, d_idx, P, dst, s));
+    src = dst;
+    for (int i = 0; i < 3; ++i) cur[i] = nxt[i];
+  }
+  for (void *t : temps) VR_HIP(hipFreeAsync(t, s));
+  VR_HIP(hipStreamSynchronize(s));  // the host contributions are borrowed by the copies
+  return VR_OK;
+  VR_GUARD_END
+}
+
+// The contributions of one resize axis, for tests: writes P (taps kept) and, if w / idx are not
+// NULL, out_len * P weights and 0-based indices.
+int vr_resize_contributions(uint64_t in_len, uint64_t out_len, int32_t *P, double *w, int32_t *idx) {
+  if (!P || !in_len || !out_len) return fail(VR_ERR_ARGUMENT, "invalid resize axis");
+  std::vector<double> ww;
+  std::vector<int32_t> ii;
+  resize_contributions(in_len, out_len, ww, ii, *P);
+  if (w) std::memcpy(w, ww.data(), ww.size() * sizeof(double));
+  if (idx) std::memcpy(idx, ii.data(), ii.size() * sizeof(int32_t));
+  return VR_OK;
+}
 
 // HenyeyGreenstein.cc:39-91 (g in [-1, 1], value at c*N*N + a*N + b)
 int vr_henyey_greenstein(uint32_t n, float g, float *out) {

@@ -238,6 +238,37 @@ def gradient_device(d_data: int, dims, d_gx: int, d_gy: int, d_gz: int, stream: 
     _lib.check(_lib.lib().vr_gradient_device(d_data, dd, d_gx, d_gy, d_gz, stream))
 
 
+def henyey_greenstein_device(n: int, g: float, d_out: int, stream: int = 0) -> None:
+    """vr_henyey_greenstein_device: HenyeyGreenstein(n, g) into device memory (n^3 floats)."""
+    check(lib().vr_henyey_greenstein_device(ctypes.c_uint32(int(n)), ctypes.c_float(g), ctypes.c_void_p(int(d_out)),
+                                            ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def normalize_device(d_in: int, n: int, new_min: float, new_max: float, d_out: int, stream: int = 0) -> None:
+    """vr_normalize_device: Volume.normalize of n single values in device memory (d_out may be d_in)."""
+    check(lib().vr_normalize_device(ctypes.c_void_p(int(d_in)), int(n), float(new_min), float(new_max),
+                                    ctypes.c_void_p(int(d_out)), ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def resize_device(d_in: int, in_dims, out_dims, d_out: int, stream: int = 0) -> None:
+    """vr_resize_device: Volume.resize (imresize3 cubic) of a column-major device volume."""
+    a = (ctypes.c_uint64 * 3)(*(list(int(x) for x in in_dims) + [1] * (3 - len(in_dims))))
+    b = (ctypes.c_uint64 * 3)(*(list(int(x) for x in out_dims) + [1] * (3 - len(out_dims))))
+    check(lib().vr_resize_device(ctypes.c_void_p(int(d_in)), a, b, ctypes.c_void_p(int(d_out)),
+                                 ctypes.c_void_p(int(stream)) if stream else None))
+
+
+def resize_contributions(in_len: int, out_len: int):
+    """(weights [out_len, P] float64, 0-based indices [out_len, P] int32) of one resize axis."""
+    P = ctypes.c_int32(0)
+    check(lib().vr_resize_contributions(int(in_len), int(out_len), ctypes.byref(P), None, None))
+    w = np.zeros((int(out_len), P.value), np.float64)
+    i = np.zeros((int(out_len), P.value), np.int32)
+    check(lib().vr_resize_contributions(int(in_len), int(out_len), ctypes.byref(P), w.ctypes.data_as(ctypes.c_void_p),
+                                        i.ctypes.data_as(ctypes.c_void_p)))
+    return w, i
+
+
 def channel(handle, t_sync, volumes, render_argv):
     """One vr_channel: handle, the 'sync_volumes' arguments after the handle (t_sync, Emission,
     Reflection, Absorption[, dx, dy, dz]) and the positional 'render' arguments after the handle.

@@ -68,9 +68,33 @@ class Volume:
         return Volume(gx), Volume(gy), Volume(gz)
 
     def normalize(self, new_min, new_max) -> None:
-        """Linear normalisation to [new_min, new_max] (Volume.m:208-220)."""
-        mx, mn = self.max(), self.min()
-        self.Data = (self._data - mn) * (new_max - new_min) / (mx - mn) + new_min
+        """Linear normalisation to [new_min, new_max] (Volume.m:208-220) in MATLAB's single
+        arithmetic: (Data - min) * single(newMax - newMin) / (max - min) + single(newMin), each step
+        rounded to single (vr_normalize_device does the same on device data)."""
+        d = self._data
+        ok = d[~np.isnan(d)]
+        mx = ok.max() if ok.size else np.float32(np.nan)
+        mn = ok.min() if ok.size else np.float32(np.nan)
+        with np.errstate(all="ignore"):
+            t = (d - mn) * np.float32(float(new_max) - float(new_min))
+            t = t / np.float32(mx - mn)
+            self.Data = t + np.float32(new_min)
+
+    def resize(self, newsize) -> None:
+        """Volume.resize (Volume.m:93-106: imresize3 for 3-D data, imresize for 2-D) on the GPU
+        (vr_resize_device: cubic, antialiasing when shrinking).  newsize: 3 (or, for 2-D data, 2)
+        sizes."""
+        import torch
+        from .mex import resize_device
+        d = self._data
+        dims = tuple(d.shape) + (1,) * (3 - d.ndim)
+        new = tuple(int(x) for x in np.asarray(newsize).reshape(-1))
+        out_dims = new + (1,) * (3 - len(new))
+        src = torch.from_numpy(np.ascontiguousarray(d.reshape(-1, order="F"))).cuda()
+        dst = torch.empty(int(np.prod(out_dims)), dtype=torch.float32, device="cuda")
+        resize_device(src.data_ptr(), dims, out_dims, dst.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        out = dst.cpu().numpy().reshape(out_dims, order="F")
+        self.Data = out if d.ndim == 3 else out.reshape(new, order="F")
 
     def pad(self, padding: int, value=0) -> None:
         """Pad all three dimensions by `padding` on both sides with `value` (Volume.m:119-135)."""
