@@ -88,6 +88,16 @@ typedef struct vr_context vr_context; /* the reference's MManager handle (mmanag
 /* 'new' (render.cpp:58-65): a persistent handle bound to the current HIP device. */
 int vr_new(vr_context **out);
 
+/* 'new' for a multi-device group (SURVEY.md 8e inside the library, so that the MATLAB classes reach
+ * every GPU of the node through the unchanged mex protocol; the reference picks one device,
+ * volumeRender.cpp:77-87).  devices[0] is the primary: 'sync_volumes' uploads there once and copies
+ * the bound volumes to the other devices over xGMI (peer copies); 'render' (and vr_render_device
+ * without a partition or counters) renders column part k of the frame (16-column blocks dealt
+ * round-robin) on devices[k], gathers the parts to the primary with peer copies and assembles the
+ * image there -- bit-identical to the one-device render.  Stereo, channels and slab launches of a
+ * group use the primary only.  A device may repeat (a rehearsal on one GPU). */
+int vr_new_multi(const int32_t *devices, int32_t n, vr_context **out);
+
 /* 'delete' (render.cpp:72-79 -> ~MManager, mmanager.hxx:103-105).  Like the reference's
  * cudaDeviceReset this frees every handle's device volumes and resets the module-global render
  * state (texture bindings, slot indices, lights, gradient method). */

@@ -9,6 +9,7 @@
 // INTEGRATION.md.  All marshalling permutations (reversed ElementSizeUm and light positions,
 // flip(R) un-flipping, [H W] order) happen inside libvrhip exactly as the reference's mex did them;
 // this file only unpacks mxArrays into the C-ABI structs of include/vrhip.h.
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -148,7 +149,18 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   if (!strcmp(cmd, "new")) {
     if (nlhs != 1) mexErrMsgTxt("New: One output expected.");
     vr_context *h = nullptr;
-    check(vr_new(&h));
+    // VR_DEVICES="0,1,...,7": every render of this handle spans those GPUs (vr_new_multi)
+    std::vector<int32_t> devs;
+    if (const char *ev = getenv("VR_DEVICES")) {
+      for (const char *q = ev; *q;) {
+        char *end = nullptr;
+        const long d = strtol(q, &end, 10);
+        if (end == q) break;
+        devs.push_back((int32_t)d);
+        q = (*end == ',') ? end + 1 : end;
+      }
+    }
+    check(devs.empty() ? vr_new(&h) : vr_new_multi(devs.data(), (int32_t)devs.size(), &h));
     mexLock();  // the module-global device state must outlive `clear functions`
     plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
     *static_cast<uint64_t *>(mxGetData(plhs[0])) = reinterpret_cast<uint64_t>(h);

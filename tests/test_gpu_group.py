@@ -1,0 +1,102 @@
+"""Multi-device groups inside the library (vr_new_multi; SURVEY.md 8e reached through the unchanged
+mex protocol): a group renders column parts on its devices and gathers them to the primary over
+xGMI.  The test box has one GPU, so the groups here repeat device 0 -- every step of the group path
+runs (replicated bindings, per-device LUT uploads and interleaved gradients, the partitioned
+launches on the children's streams, the part gathers and the assembly), with VR_GROUP_REPLICATE=1
+the volume replicas are real copies too -- and every image must equal the one-device render bit for
+bit, frame after frame, as the camera, the lights and the data change."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+vr = pytest.importorskip("volume_renderer_amd")
+torch = pytest.importorskip("torch")
+from volume_renderer_amd import mex  # noqa: E402
+
+
+def _scene(r, v, lit=True):
+    if lit:
+        r.VolumeIllumination = vr.Volume(vr.HenyeyGreenstein(32))
+        r.LightSources = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+    r.FocalLength, r.DistanceToObject, r.OpacityThreshold = 3.0, 6, 0.9
+    r.rotate(125, 25, 0)
+    r.ImageResolution = [150, 97]
+    r.VolumeEmission = v
+    r.VolumeAbsorption = v
+    r.FactorAbsorption, r.FactorReflection = 0.6, 0.4
+    r.Color = [1, 1, 0]
+    return r
+
+
+@pytest.mark.parametrize("devices,replicate", [("0,0", "0"), ("0,0,0", "1"), ("0,0,0,0,0,0,0,0", "1")])
+@pytest.mark.parametrize("grad", ["compute", "lookup"])
+def test_group_render_equals_one_device(monkeypatch, counter_clock, devices, replicate, grad):
+    monkeypatch.setenv("VR_GROUP_REPLICATE", replicate)
+    data = [O.shell_volume(48), np.asfortranarray(O.shell_volume(48)[::-1] * np.float32(0.7))]
+
+    def frames(group):
+        if group:
+            monkeypatch.setenv("VR_DEVICES", devices)
+        else:
+            monkeypatch.delenv("VR_DEVICES", raising=False)
+        r = vr.VolumeRender()
+        v = vr.Volume(data[0])
+        _scene(r, v)
+        if grad == "lookup":
+            r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
+        out = [r.render()]
+        r.rotate(0, 20, 0)                                   # camera change
+        out.append(r.render())
+        r.LightSources = [vr.LightSource([-200, 100, 900], [0.3, 1, 0.2])]  # lights change
+        out.append(r.render())
+        r.VolumeEmission.Data = data[1]                      # data change (re-sync, replicas refreshed)
+        if grad == "lookup":
+            r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = r.VolumeEmission.grad()
+        out.append(r.render())
+        monkeypatch.delenv("VR_DEVICES", raising=False)
+        r.delete()
+        return out
+
+    one = frames(False)
+    grp = frames(True)
+    for k, (a, b) in enumerate(zip(one, grp)):
+        assert a.max() > 0
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+
+
+def test_group_render_device_on_a_stream(monkeypatch, counter_clock):
+    """vr_render_device on a group handle: the assembled image in device memory on the caller's
+    stream, several frames in flight."""
+    monkeypatch.setenv("VR_GROUP_REPLICATE", "1")
+    n, W, H = 64, 200, 120
+    t = torch.empty(n ** 3, dtype=torch.float32, device="cuda")
+    mex.synth_shell_device(t.data_ptr(), n)
+    torch.cuda.synchronize()
+    em = mex.DeviceVolume(t.data_ptr(), (n, n, n), last_update=3, owner=t)
+    refl = vr.Volume(1)
+    refl.TimeLastUpdate = np.uint64(2)
+    lut = vr.Volume(vr.HenyeyGreenstein(64))
+    lut.TimeLastUpdate = np.uint64(4)
+    lights = [vr.LightSource([500, 1000, 550], [0, 1, 1])]
+    R = np.flip(O.rotation(125, 25, 0), 0).astype(np.float32)
+    argv = (lights, lut, np.float32([1, 0.4, 0.6]), np.float32([1, 1, 1]), np.uint64([H, W]), R,
+            np.float32([0, 3, 6]), np.float32(0.9), np.float32([1, 1, 0]))
+    h1 = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h1, np.uint64(0), em, refl, em)
+    want = vr.volumeRender("render", h1, *argv).reshape(-1, order="F")
+    monkeypatch.setenv("VR_DEVICES", "0,0,0,0")
+    h = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)
+    ra, keep = mex.render_args(*argv)
+    s = torch.cuda.Stream()
+    outs = [torch.empty(3 * W * H, dtype=torch.float32, device="cuda") for _ in range(4)]
+    for o in outs:
+        mex.render_device(h, ra, o.data_ptr(), None, 0, s.cuda_stream)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    vr.volumeRender("delete", h)
+    vr.volumeRender("delete", h1)

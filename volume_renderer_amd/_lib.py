@@ -64,6 +64,7 @@ _lib = None
 # (name, restype, argtypes) for every symbol of include/vrhip.h
 SIGNATURES = [
     ("vr_new", c_int, [POINTER(c_void_p)]),
+    ("vr_new_multi", c_int, [POINTER(c_int32), c_int32, POINTER(c_void_p)]),
     ("vr_delete", c_int, [c_void_p]),
     ("vr_mem_info", c_int, [c_void_p, c_char_p, c_size_t]),
     ("vr_sync_volumes", c_int, [c_void_p, c_uint64, POINTER(VrVolume), POINTER(VrVolume), POINTER(VrVolume),

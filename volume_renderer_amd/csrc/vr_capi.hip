@@ -147,6 +147,9 @@ struct DevBuf {
   // completion of the last launch that reads it (vr_resources.h): it is neither rewritten nor freed
   // before then
   vr_host::EventPtr last_use;
+  // multi-device group (vr_new_multi): its copies on the other devices, and the version each copies
+  std::map<int, std::shared_ptr<DevBuf>> replicas;
+  std::map<int, uint64_t> replica_of;
   ~DevBuf() { vr_host::pooled_free(ptr, bytes, device, last_use); }
 };
 using BufPtr = std::shared_ptr<DevBuf>;
@@ -179,6 +182,16 @@ struct vr_context {
   int32_t snap_idx[3] = {0, 0, 0};
   int32_t snap_grad = 0;
   bool has_snap = false;
+  // multi-device group (vr_new_multi, SURVEY.md 8e inside the library): the primary (this handle,
+  // the API's) holds one child per further device; each child renders a column partition of the
+  // frame with replicas of the primary's bound volumes on its device, and its part is gathered
+  // to the primary over xGMI (peer copies) and assembled there
+  std::vector<vr_context *> children;
+  vr_context *parent = nullptr;
+  hipStream_t gstream = nullptr;  // child: its device's stream (replica copies, render, gather)
+  hipEvent_t gdone = nullptr;     // child: its part has landed on the primary
+  float *d_part = nullptr;        // child: its part image; primary: all parts
+  size_t d_part_bytes = 0;
 };
 
 namespace {
@@ -193,13 +206,18 @@ struct TexUnit {
                                                          // per launch (vr_host::LaunchRec::stage)
   // lookup gradient, interleaved (gx, gy, gz, 0) per padded voxel, built from the bound gradient
   // textures when their dims equal the emission's; rebuilt when any of them changes
-  std::shared_ptr<DevBuf> gvec;
-  const DevBuf *gvec_src[3] = {nullptr, nullptr, nullptr};
-  uint64_t gvec_ver[3] = {0, 0, 0};
+  struct GVec {
+    std::shared_ptr<DevBuf> buf;
+    const DevBuf *src[3] = {nullptr, nullptr, nullptr};
+    uint64_t ver[3] = {0, 0, 0};
+  };
+  std::map<int, GVec> gvec;  // per device (a multi-device group renders on every device)
 };
 
 std::mutex g_mu;
 TexUnit g_tex;
+uint64_t g_version = 0;
+uint64_t next_version() { return ++g_version; }
 std::set<vr_context *> g_contexts;
 
 struct DeviceGuard {
@@ -216,8 +234,7 @@ struct DeviceGuard {
 
 void reset_tex_unit() {
   for (auto &b : g_tex.bind) b.reset();
-  g_tex.gvec.reset();
-  for (int i = 0; i < 3; ++i) g_tex.gvec_src[i] = nullptr;
+  g_tex.gvec.clear();
   g_tex.idx_em = T_EM;
   g_tex.idx_ab = T_EM;
   g_tex.idx_re = T_RE;
@@ -268,8 +285,7 @@ void sync_volume(vr_context *h, int tex, int slot) {
     b->nonfinite = st.nonfinite != 0;
     b->maxabs = st.maxabs;
   }
-  static uint64_t s_version = 0;
-  b->version = ++s_version;
+  b->version = next_version();
   b->src_data = v.data;
   b->src_last_update = v.last_update;
   b->src_bytes = v.memory_size;
@@ -613,7 +629,8 @@ using LaunchRec = vr_host::LaunchRec<BufPtr>;
 void bind_reads(LaunchRec &L) {
   for (const BufPtr &b : g_tex.bind)
     if (b) L.reads.push_back(b);
-  if (g_tex.gvec) L.reads.push_back(g_tex.gvec);
+  for (const auto &kv : g_tex.gvec)
+    if (kv.second.buf && kv.first == L.device) L.reads.push_back(kv.second.buf);
 }
 void stage_frame(LaunchRec &L, vr::RenderParams &P, const std::vector<vr::DevLight> &lights) {
   const void *d = nullptr;
@@ -758,28 +775,29 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     // interleave the three gradient textures (one 16-byte load per voxel instead of three 4-byte
     // gathers from three volumes); without memory for it the kernel gathers them separately
     const BufPtr &bx = g_tex.bind[T_DX], &by = g_tex.bind[T_DY], &bz = g_tex.bind[T_DZ];
-    bool fresh = g_tex.gvec && g_tex.gvec->device == h->device;
+    TexUnit::GVec &G = g_tex.gvec[h->device];
+    bool fresh = G.buf != nullptr;
     const DevBuf *src[3] = {bx.get(), by.get(), bz.get()};
-    for (int i = 0; i < 3 && fresh; ++i) fresh = g_tex.gvec_src[i] == src[i] && g_tex.gvec_ver[i] == src[i]->version;
+    for (int i = 0; i < 3 && fresh; ++i) fresh = G.src[i] == src[i] && G.ver[i] == src[i]->version;
     if (!fresh) {
-      g_tex.gvec.reset();
+      G.buf.reset();
       const uint64_t n = bx->bytes / sizeof(float);
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
       gv->bytes = n * 4 * sizeof(float);
       if (vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device) == hipSuccess) {
         VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
-        g_tex.gvec = gv;
+        G.buf = gv;
         for (int i = 0; i < 3; ++i) {
-          g_tex.gvec_src[i] = src[i];
-          g_tex.gvec_ver[i] = src[i]->version;
+          G.src[i] = src[i];
+          G.ver[i] = src[i]->version;
         }
       } else {
         (void)hipGetLastError();
         gv->ptr = nullptr;
       }
     }
-    if (g_tex.gvec) P.gvec = g_tex.gvec->ptr;
+    if (G.buf) P.gvec = G.buf->ptr;
   }
   if (fusable && march && F.mode <= 1 && !F.big && !P.steps) {
     *fusable = 1;
@@ -946,6 +964,133 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   return VR_OK;
 }
 
+// ---- multi-device group (vr_new_multi) ----------------------------------------------------------
+
+// The copy of buffer b on device `dev`, refreshed when b was re-uploaded since (peer copy over xGMI on
+// the device's group stream; a replica a launch still reads is replaced, not overwritten).
+BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
+  if (!b) return b;
+  if (b->device == dev && !env_flag("VR_GROUP_REPLICATE")) return b;  // test switch: copy on one device too
+  BufPtr &r = b->replicas[dev];
+  if (r && r->bytes == b->bytes && b->replica_of[dev] == b->version) return r;
+  if (!(r && r->bytes == b->bytes && vr_host::done(r->last_use))) {
+    r = std::make_shared<DevBuf>();
+    r->device = dev;
+    r->bytes = b->bytes;
+    if (b->bytes) {
+      DeviceGuard dg(dev);
+      VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&r->ptr), b->bytes, dev));
+    }
+  }
+  if (b->bytes) VR_HIP(hipMemcpyPeerAsync(r->ptr, dev, b->ptr, b->device, b->bytes, s));
+  for (int i = 0; i < 3; ++i) r->dims[i] = b->dims[i];
+  r->nonfinite = b->nonfinite;
+  r->maxabs = b->maxabs;
+  r->src_data = b->src_data;
+  r->src_last_update = b->src_last_update;
+  r->src_bytes = b->src_bytes;
+  r->version = next_version();
+  b->replica_of[dev] = b->version;
+  return r;
+}
+
+void enable_peer(int a, int b) {
+  if (a == b) return;
+  int ok = 0;
+  if (hipDeviceCanAccessPeer(&ok, a, b) == hipSuccess && ok) {
+    DeviceGuard dg(a);
+    const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+    if (e != hipSuccess) (void)hipGetLastError();  // already enabled / unsupported: copies still work
+  }
+}
+
+// After a sync of the primary: the children record the same volumes, and the bound volumes are
+// copied to their devices now (one H2D to the primary, then peer copies), not in the render.
+void group_sync(vr_context *h) {
+  for (vr_context *c : h->children) {
+    DeviceGuard dg(c->device);
+    for (int t = 0; t < T_COUNT; ++t) c->vol[t] = h->vol[t];
+    c->time_last_mem_sync = h->time_last_mem_sync;
+    for (int t = 0; t < T_COUNT; ++t)
+      if (t != T_LIGHT && g_tex.bind[t]) (void)replicate(g_tex.bind[t], c->device, c->gstream);
+  }
+}
+
+// 'render' on a group: child k renders column part k (16-column blocks dealt round-robin, as
+// bench.py's ranks), the primary part 0; the children's parts are peer-copied into the primary's
+// part buffer and assembled there into d_out (the primary's device, on `stream`).  The module-global
+// bindings are the primary's again when this returns.
+int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream_t stream) {
+  const int n = 1 + (int)h->children.size();
+  const int32_t bc = 16;
+  const int64_t W = (int64_t)a->resolution[1], H = (int64_t)a->resolution[0];
+  vr_partition p0{bc, 0, n, 0};
+  const int64_t maxc = part_columns(W, bc, 0, n);
+  const size_t part_floats = (size_t)maxc * (size_t)H * 3;
+  if (!part_floats) {
+    Frame F;
+    return do_render(h, a, nullptr, d_out, nullptr, stream, F);
+  }
+  if (h->d_part_bytes < (size_t)n * part_floats * sizeof(float)) {
+    if (h->d_part) VR_HIP(hipFree(h->d_part));
+    h->d_part = nullptr;
+    h->d_part_bytes = 0;
+    VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&h->d_part), (size_t)n * part_floats * sizeof(float)));
+    h->d_part_bytes = (size_t)n * part_floats * sizeof(float);
+  }
+  // the primary's part first: it uploads the frame's lights / LUT and binds them
+  Frame F0;
+  int rc = do_render(h, a, &p0, h->d_part, nullptr, stream, F0);
+  if (rc) return rc;
+  BufPtr saved[T_COUNT];
+  for (int t = 0; t < T_COUNT; ++t) saved[t] = g_tex.bind[t];
+  for (int k = 1; k < n; ++k) {
+    vr_context *c = h->children[k - 1];
+    DeviceGuard dg(c->device);
+    if (c->d_part_bytes < part_floats * sizeof(float)) {
+      if (c->d_part) VR_HIP(hipFree(c->d_part));
+      c->d_part = nullptr;
+      c->d_part_bytes = 0;
+      VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&c->d_part), part_floats * sizeof(float)));
+      c->d_part_bytes = part_floats * sizeof(float);
+    }
+    for (int t = 0; t < T_COUNT; ++t) c->vol[t] = h->vol[t];
+    for (int t = 0; t < T_COUNT; ++t)  // the LUT: the child's own upload (do_render keeps it resident)
+      g_tex.bind[t] = t == T_LIGHT ? c->buf[T_LIGHT] : replicate(saved[t], c->device, c->gstream);
+    vr_partition pk{bc, k, n, 0};
+    Frame F;
+    rc = do_render(c, a, &pk, c->d_part, nullptr, c->gstream, F);
+    if (rc) break;
+    // the previous frame's assembly has read this slot of the primary's part buffer
+    VR_HIP(hipStreamWaitEvent(c->gstream, h->gdone, 0));
+    VR_HIP(hipMemcpyPeerAsync(h->d_part + (size_t)k * part_floats, h->device, c->d_part, c->device,
+                              part_floats * sizeof(float), c->gstream));
+    VR_HIP(hipEventRecord(c->gdone, c->gstream));
+  }
+  for (int t = 0; t < T_COUNT; ++t) g_tex.bind[t] = saved[t];
+  if (rc) return rc;
+  for (vr_context *c : h->children) VR_HIP(hipStreamWaitEvent(stream, c->gdone, 0));
+  VR_HIP(vr::launch_assemble(h->d_part, W, H, bc, n, maxc, d_out, stream));
+  VR_HIP(hipEventRecord(h->gdone, stream));
+  return VR_OK;
+}
+
+void delete_children(vr_context *h) {
+  for (vr_context *c : h->children) {
+    DeviceGuard dg(c->device);
+    (void)hipStreamSynchronize(c->gstream);
+    for (auto &b : c->buf) b.reset();
+    if (c->d_part) (void)hipFree(c->d_part);
+    if (c->d_out) (void)hipFree(c->d_out);
+    free_schedules(c);
+    free_views(c);
+    if (c->gdone) (void)hipEventDestroy(c->gdone);
+    if (c->gstream) (void)hipStreamDestroy(c->gstream);
+    delete c;
+  }
+  h->children.clear();
+}
+
 #define VR_GUARD_BEGIN try {
 #define VR_GUARD_END                                                                             \
   }                                                                                              \
@@ -1036,6 +1181,37 @@ int vr_new(vr_context **out) {
   VR_GUARD_END
 }
 
+int vr_new_multi(const int32_t *devices, int32_t n, vr_context **out) {
+  if (!out) return fail(VR_ERR_ARGUMENT, "New: One output expected.");
+  if (!devices || n < 1) return fail(VR_ERR_ARGUMENT, "no devices");
+  std::lock_guard<std::mutex> lk(g_mu);
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) return fail(VR_ERR_DEVICE, "no HIP device");
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= count) return fail(VR_ERR_ARGUMENT, "invalid device index");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(devices[0]);
+  vr_context *h = new vr_context();
+  h->device = devices[0];
+  VR_HIP(hipEventCreateWithFlags(&h->gdone, hipEventDisableTiming));
+  for (int i = 1; i < n; ++i) {
+    enable_peer(devices[0], devices[i]);
+    enable_peer(devices[i], devices[0]);
+    DeviceGuard dk(devices[i]);
+    vr_context *c = new vr_context();
+    c->device = devices[i];
+    c->parent = h;
+    h->children.push_back(c);
+    VR_HIP(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+    VR_HIP(hipEventCreateWithFlags(&c->gdone, hipEventDisableTiming));
+  }
+  g_contexts.insert(h);
+  *out = h;
+  g_last_error.clear();
+  return VR_OK;
+  VR_GUARD_END
+}
+
 int vr_delete(vr_context *h) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
@@ -1043,6 +1219,8 @@ int vr_delete(vr_context *h) {
   // ~MManager -> cudaDeviceReset(): every handle's device memory and the module globals go.
   reset_tex_unit();
   for (vr_context *c : g_contexts) {
+    for (vr_context *k : c->children)  // a group's children: their buffers go with the device reset
+      for (auto &b : k->buf) b.reset();
     for (auto &b : c->buf) b.reset();
     if (c->d_out) (void)hipFree(c->d_out);
     c->d_out = nullptr;
@@ -1050,6 +1228,9 @@ int vr_delete(vr_context *h) {
     free_schedules(c);
     free_views(c);
   }
+  delete_children(h);
+  if (h->gdone) (void)hipEventDestroy(h->gdone);
+  if (h->d_part) (void)hipFree(h->d_part);
   g_contexts.erase(h);
   h->signature = 0;
   delete h;
@@ -1160,7 +1341,12 @@ int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume 
                     const vr_volume *reflection, const vr_volume *absorption, const vr_volume *dx,
                     const vr_volume *dy, const vr_volume *dz) {
   std::lock_guard<std::mutex> lk(g_mu);
-  return do_sync_volumes(h, time_last_mem_sync, emission, reflection, absorption, dx, dy, dz);
+  const int rc = do_sync_volumes(h, time_last_mem_sync, emission, reflection, absorption, dx, dy, dz);
+  if (rc || h->children.empty()) return rc;
+  VR_GUARD_BEGIN
+  group_sync(h);
+  return VR_OK;
+  VR_GUARD_END
 }
 
 // Multi-channel render (vr_render_channels): channel i is what vr_sync_volumes +
@@ -1349,7 +1535,8 @@ int vr_render(vr_context *h, const vr_render_args *a, float *out) {
     h->d_out_bytes = bytes;
   }
   Frame F;
-  int rc = do_render(h, a, nullptr, h->d_out, nullptr, nullptr, F);
+  int rc = h->children.empty() ? do_render(h, a, nullptr, h->d_out, nullptr, nullptr, F)
+                               : group_render(h, a, h->d_out, nullptr);
   if (rc) return rc;
   if (bytes) VR_HIP(hipMemcpy(out, h->d_out, bytes, hipMemcpyDeviceToHost));
   return VR_OK;
@@ -1401,6 +1588,7 @@ int vr_render_device(vr_context *h, const vr_render_args *a, const vr_partition 
   VR_GUARD_BEGIN
   DeviceGuard dg(h->device);
   vr_host::prune_retired();  // buffers whose last launch has completed
+  if (!h->children.empty() && !part && !d_steps) return group_render(h, a, d_out, (hipStream_t)stream);
   Frame F;
   return do_render(h, a, part, d_out, d_steps, (hipStream_t)stream, F);
   VR_GUARD_END

@@ -319,6 +319,13 @@ def sum_channels_device(d_in: int, n: int, views: int, image_floats: int, d_out:
                                        ctypes.c_void_p(int(d_out)), ctypes.c_void_p(int(stream)) if stream else None))
 
 
+def _group_devices():
+    """VR_DEVICES (comma-separated device indices, primary first) selects multi-device handles."""
+    import os
+    ev = os.environ.get("VR_DEVICES", "").strip()
+    return [int(x) for x in ev.split(",") if x.strip()] if ev else []
+
+
 def volumeRender(cmd, *args):
     """The `volumeRender` mex: commands 'new', 'delete', 'mem_info', 'sync_volumes', 'render'."""
     nrhs = 1 + len(args)
@@ -327,7 +334,12 @@ def volumeRender(cmd, *args):
     L = lib()
     if cmd == "new":
         p = ctypes.c_void_p()
-        check(L.vr_new(ctypes.byref(p)))
+        devs = _group_devices()
+        if devs:  # VR_DEVICES="0,1,...": a multi-device group (vr_new_multi), as the MEX adaptor does
+            arr = (ctypes.c_int32 * len(devs))(*devs)
+            check(L.vr_new_multi(arr, len(devs), ctypes.byref(p)))
+        else:
+            check(L.vr_new(ctypes.byref(p)))
         return np.uint64(p.value)
     if cmd == "render_channels":  # vr_render_channels: ('render_channels', channels[, stereo, base])
         return render_channels(*args)
