@@ -21,6 +21,17 @@
  *     w = rint(frac(xB)*256)/256 (9-bit fixed-point weights, 8 fractional bits), taps clamped to
  *     [0, N-1]; lerp(a, b, w) = fma(w, b - a, a), order x -> y -> z.  A NaN coordinate is treated
  *     as 0.  An unbound texture reads 0.
+ *
+ * Assumption variants (tools/parity_band.py): the reference's output depends on
+ * details this image cannot observe; each -D switch below replaces one assumption by a plausible
+ * alternative so that the spread of "equally faithful" fp32 renders can be measured:
+ *   OR_VAR_TRUNC      8-bit filter weights by truncation instead of round-to-nearest-even
+ *   OR_VAR_AXIS_FMA   the sampler's c*N - 0.5 as one fused multiply-add
+ *   OR_VAR_LERP_2MUL  the CUDA guide's filter formula (1 - w)*a + w*b instead of fma(w, b - a, a)
+ *   OR_VAR_NOFMA      no contraction anywhere (nvcc --fmad=false)
+ *   OR_VAR_RSQRT_CR   helper_math normalize with a correctly rounded rsqrt instead of 1/sqrtf
+ *   OR_VAR_EXP2       __expf as exp2f(x * log2 e) (the intrinsic's formulation) instead of expf
+ *   OR_VAR_NAN_PROP   a NaN texture coordinate makes the fetch NaN instead of sampling at 0
  */
 #include <math.h>
 #include <stdint.h>
@@ -28,6 +39,10 @@
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
+#endif
+
+#ifdef OR_VAR_NOFMA
+#define FMA_IMPL(a, b, c) ((a) * (b) + (c))
 #endif
 
 #ifdef OR_DOUBLE
@@ -41,7 +56,11 @@ typedef double real;
 #define OR_SUFFIX(name) name##_f64
 #else
 typedef float real;
+#ifdef OR_VAR_NOFMA
+#define FMA(a, b, c) FMA_IMPL(a, b, c)
+#else
 #define FMA fmaf
+#endif
 #define SQRT sqrtf
 #define EXP expf
 #define ACOS acosf
@@ -95,16 +114,28 @@ static inline real dot3(vec3 a, vec3 b) { return FMA(a.z, b.z, FMA(a.y, b.y, a.x
 static inline real len3(vec3 a) { return SQRT(dot3(a, a)); }
 /* helper_math.h normalize(v) = v * rsqrtf(dot(v,v)); rsqrtf modelled as 1/sqrtf. */
 static inline vec3 normalize3(vec3 a) {
+#ifdef OR_VAR_RSQRT_CR
+  real inv = (real)(1.0 / sqrt((double)dot3(a, a)));
+#else
   real inv = (real)1 / SQRT(dot3(a, a));
+#endif
   return v3(a.x * inv, a.y * inv, a.z * inv);
 }
 
 /* One axis of the CUDA linear-filter address computation (normalized coords, clamp). */
 static inline real tex_axis(real c, int64_t n, int64_t *i0, int64_t *i1) {
   if (c != c) c = (real)0; /* NaN coordinate -> 0 (assumption) */
+#ifdef OR_VAR_AXIS_FMA
+  real xb = FMA(c, (real)n, (real)-0.5);
+#else
   real xb = c * (real)n - (real)0.5;
+#endif
   real fl = FLOOR(xb);
+#ifdef OR_VAR_TRUNC
+  real w = FLOOR((xb - fl) * (real)256) * ((real)1 / (real)256);
+#else
   real w = RINT((xb - fl) * (real)256) * ((real)1 / (real)256);
+#endif
   int64_t i = (int64_t)fl;
   int64_t a = i, b = i + 1;
   *i0 = a < 0 ? 0 : (a > n - 1 ? n - 1 : a);
@@ -112,11 +143,18 @@ static inline real tex_axis(real c, int64_t n, int64_t *i0, int64_t *i1) {
   return w;
 }
 
+#ifdef OR_VAR_LERP_2MUL
+static inline real lerp(real a, real b, real w) { return ((real)1 - w) * a + w * b; }
+#else
 static inline real lerp(real a, real b, real w) { return FMA(w, b - a, a); }
+#endif
 
 /* tex3D(tex, x, y, z) on a bound fp32 texture, volumeRender_kernel.cu:544-548 semantics. */
 static real tex3d(const or_tex *t, real x, real y, real z) {
   if (!t->data) return (real)0; /* unbound texture reference reads 0 (assumption) */
+#ifdef OR_VAR_NAN_PROP
+  if (x != x || y != y || z != z) return (real)NAN;
+#endif
   int64_t x0, x1, y0, y1, z0, z1;
   real wx = tex_axis(x, t->nx, &x0, &x1);
   real wy = tex_axis(y, t->ny, &y0, &y1);
@@ -242,7 +280,11 @@ static uint64_t render_pixel(const or_params *P, int64_t x, int64_t y, real rgb[
                     : tex3d(&P->ab, ps.x, ps.y, ps.z);
     real e = Fe * em_s;
     real a = Fa * ab_s;
+#ifdef OR_VAR_EXP2
+    real alpha = (real)1 - exp2f((-a * tstep) * 0x1.715476p+0f);
+#else
     real alpha = (real)1 - EXP(-a * tstep);
+#endif
     real eds = e * tstep;
     vec3 ill = v3(0, 0, 0);
     /* shade() runs unconditionally in the reference; with no lights its result is exactly 0

@@ -210,3 +210,22 @@ def test_golden_fixtures(name):
     assert np.array_equal(img.view(np.uint32), data["image"].view(np.uint32))
     img64, _ = G.oracle_render(name, double=True)
     assert np.array_equal(img64.view(np.uint32), data["image64"].view(np.uint32))
+
+
+def test_assumption_variants_build_and_differ():
+    """The oracle's assumption variants (oracle/variants/, tools/parity_band.py) load and render;
+    truncating filter weights moves the EA-only 64^3 image far outside the fp32 envelope, a fused
+    sampler coordinate changes nothing on a power-of-two grid (c*N is exact there)."""
+    import golden_cases as G
+    sc = G.SCENES["c1_ea_64"]
+    S = O.OracleSession()
+    h = S.new()
+    v = O.OVolume(sc["em"](), G.STAMP_EM)
+    S.sync_volumes(h, 0, v, O.OVolume(np.ones((1, 1), np.float32), G.STAMP_RE), v)
+    args = G.render_argv(sc, None, None)[2:]
+    base, _ = S.render(h, None, None, *args, threads=4)
+    vdir = os.path.join(os.path.dirname(O.LIB_PATH), "variants")
+    trunc, _ = S.render(h, None, None, *args, threads=4, lib_path=os.path.join(vdir, "liboracle_trunc.so"))
+    fused, _ = S.render(h, None, None, *args, threads=4, lib_path=os.path.join(vdir, "liboracle_axis_fma.so"))
+    assert np.isfinite(trunc).all() and np.abs(trunc - base).max() > 1e-4 * base.max()
+    assert np.array_equal(fused.view(np.uint32), base.view(np.uint32))
