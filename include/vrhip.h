@@ -193,23 +193,27 @@ int vr_assemble_partitions(const float *d_parts, int64_t w, int64_t h, int32_t b
 
 /* --- sort-last slabs (volumes larger than one GPU; no MATLAB counterpart: the
  * reference aborts when a volume does not fit, mmanager.hxx:144-173) ----------------------------
- * The handle's synced emission volume holds planes [z_first, z_first + d2) of a volume of depth
- * `depth` (d0, d1 as synced).  The render marches every ray of the full W x H image over the
+ * The bound emission volume (the last vr_sync_volumes on any handle, as for vr_render) holds
+ * planes [z_first, z_first + d2) of a volume of depth `depth` (d0, d1 as synced).  The render marches every ray of the full W x H image over the
  * samples it owns, those with z0 <= p.z * depth < z1 (p the normalized sample position; z0 = -inf
  * / z1 = +inf for the end slabs), with positions, step counts and early exit exactly as the
  * one-volume march.  part (NULL = the whole image) restricts the render to the columns of an
- * image partition (the tiles of a pipelined multi-GPU sweep).  Ray state: five planes of
- * cols*H floats, [c][local column][y] = premultiplied r, g, b, alpha, and 1 if the ray continues
- * past this slab (cols = vr_partition_columns); d_state_in NULL = fresh rays, may equal
+ * image partition (the tiles of a pipelined multi-GPU sweep).  Ray state: VR_SLAB_PLANES planes
+ * of cols*H floats, [c][local column][y] (cols = vr_partition_columns): premultiplied r, g, b,
+ * alpha; 1 if the ray continues past this slab; and for such a ray its resume point -- t, the
+ * position x, y, z and the sample index (int32 bits) of its next sample -- from which the next
+ * slab continues the march without replaying it.  d_state_in NULL = fresh rays, may equal
  * d_state_out.  direction +1 handles the rays with dir.z >= 0 (run the slabs in ascending z),
- * -1 those with dir.z < 0 (descending); other rays pass through.  Chaining both sweeps over all
+ * -1 those with dir.z < 0 (descending), 0 both (the top slab, where the descending rays start:
+ * its ascending launch marches them too); other rays pass through.  Chaining both sweeps over all
  * slabs gives the one-volume image bit for bit in the first three planes.  Compute gradient or
  * emission-absorption only; absorption must alias emission (the reference's default). */
+#define VR_SLAB_PLANES 10
 typedef struct vr_slab {
   uint64_t depth;    /* global depth D of the emission volume                          */
   uint64_t z_first;  /* global index of the first synced plane                         */
   double z0, z1;     /* owned range of p.z * D                                         */
-  int32_t direction; /* +1 / -1                                                         */
+  int32_t direction; /* +1 / -1 / 0                                                     */
   int32_t reserved;
 } vr_slab;
 int vr_render_slab(vr_context *h, const vr_render_args *args, const vr_slab *slab, const vr_partition *part,

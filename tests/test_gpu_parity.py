@@ -454,16 +454,21 @@ def test_unchanged_lut_and_gradients_stay_resident(monkeypatch, counter_clock):
     r.delete()
 
 
-def _slab_chain(data, es, bounds, lights, lut, ra_args, W, H, shade):
+def _slab_chain(data, es, bounds, lights, lut, ra_args, W, H, merged=True):
     """Render `data` as len(bounds)-1 z-slabs, each synced on its own (only its planes resident):
-    the ascending sweep over the slabs, then the descending one, chaining the ray state."""
+    the ascending sweep over the slabs, then the descending one, chaining the ray state (merged:
+    the top slab marches the descending rays in its ascending launch, direction 0, as
+    parallel.sort_last_sweeps does; otherwise it runs both sweeps)."""
     import torch
     from volume_renderer_amd import mex
     D = data.shape[2]
-    state = torch.zeros(5 * W * H, dtype=torch.float32, device="cuda")
+    state = torch.zeros(mex.SLAB_PLANES * W * H, dtype=torch.float32, device="cuda")
     ra, keep = mex.render_args(lights, lut, *ra_args)
     nslab = len(bounds) - 1
-    order = [(s, +1) for s in range(nslab)] + [(s, -1) for s in reversed(range(nslab))]
+    if merged:
+        order = [(s, +1 if s < nslab - 1 else 0) for s in range(nslab)] + [(s, -1) for s in reversed(range(nslab - 1))]
+    else:
+        order = [(s, +1) for s in range(nslab)] + [(s, -1) for s in reversed(range(nslab))]
     for i, (s, direction) in enumerate(order):
         z0, z1 = bounds[s], bounds[s + 1]
         first, count = mex.slab_planes(data.shape, es, z0, z1)
@@ -474,30 +479,47 @@ def _slab_chain(data, es, bounds, lights, lut, ra_args, W, H, shade):
                         state.data_ptr())
         torch.cuda.synchronize()
         vr.volumeRender("delete", h)
-    st = state.view(5, W, H).cpu().numpy()
+    st = state.view(mex.SLAB_PLANES, W, H).cpu().numpy()
     return np.ascontiguousarray(np.transpose(st[:3], (2, 1, 0))), st  # [H, W, 3]
+
+
+def _slab_case(case):
+    if case == "cube3":
+        return O.shell_volume(48), [1, 1, 1], [-np.inf, 17, 31, np.inf]
+    if case == "one":  # a single slab: one launch marches every ray (direction 0)
+        return O.shell_volume(48), [1, 1, 1], [-np.inf, np.inf]
+    if case == "pow2":  # a power-of-two cube: the fast variant's half-texel taps; thin slabs
+        return O.shell_volume(64), [1, 1, 1], [-np.inf, 20, 21.5, 22, 40, np.inf]
+    if case == "gap":  # empty planes up to just before a boundary (and after the next): the staged
+        # boxes there are all zero, and an empty-chunk leap must not carry a ray into the next slab
+        d = O.shell_volume(48).copy(order="F")
+        d[:, :, :24] = 0
+        d[:, :, 37:] = 0
+        return d, [1, 1, 1], [-np.inf, 26, 35, np.inf]
+    # anisotropic element size and depth: the gradient taps reach further than +-0.5 plane; a slab
+    # thinner than a step is crossed without an owned sample by some rays
+    data = np.asfortranarray(O.shell_volume(48)[:, :40, :])
+    data = np.asfortranarray(np.concatenate([data, data[:, :, ::-1]], axis=2)[:, :, :70])
+    return data, [2.0, 1.0, 1.0], [-np.inf, 12.5, 30, 30.2, 51, np.inf]
 
 
 @pytest.mark.parametrize("lanes", ["1", "2", "4"])
 @pytest.mark.parametrize("shade", ["fast", "exact"])
-@pytest.mark.parametrize("case", ["cube3", "aniso4"])
-def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case, shade, lanes):
+@pytest.mark.parametrize("case,merged", [("cube3", True), ("cube3", False), ("aniso5", True), ("one", True),
+                                         ("pow2", True), ("gap", True)])
+def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case, merged, shade, lanes):
     """Sort-last bricks: a volume split into z-slabs, each rendered with only
     its own planes resident, composited by passing the exact ray state from slab to slab in ray
-    order (ascending z for rays with dir.z >= 0, descending for the others) gives the one-volume
-    image bit for bit -- same sample positions, step counts and early exits -- with any depth
-    lanes in the slab launches."""
+    order (ascending z for rays with dir.z >= 0, descending for the others), each slab resuming the
+    march at the ray's next sample, gives the one-volume image bit for bit -- same sample
+    positions, step counts and early exits -- with any depth lanes in the slab launches.  The chain
+    is also checked against the oracle's render of the whole volume (SURVEY.md 8c tolerance)."""
     monkeypatch.setenv("VR_DEPTH_LANES", lanes)
     if shade == "exact":
         monkeypatch.setenv("VR_EXACT_SHADE", "1")
     else:
         monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
-    if case == "cube3":
-        data, es, bounds = O.shell_volume(48), [1, 1, 1], [-np.inf, 17, 31, np.inf]
-    else:  # anisotropic element size and depth: the gradient taps reach further than +-0.5 plane
-        data = np.asfortranarray(O.shell_volume(48)[:, :40, :])
-        data = np.asfortranarray(np.concatenate([data, data[:, :, ::-1]], axis=2)[:, :, :70])
-        es, bounds = [2.0, 1.0, 1.0], [-np.inf, 12.5, 30, 51, np.inf]
+    data, es, bounds = _slab_case(case)
     W, H = 88, 72
     v = vr.Volume(data)
     r = ex1_renderer(v, res=(W, H))
@@ -509,11 +531,44 @@ def test_sort_last_slabs_match_the_whole_volume(monkeypatch, counter_clock, case
     ra_args = (np.float32([1.0, 0.4, 0.6]), np.float32(es), np.uint64([H, W]),
                np.flip(r.RotationMatrix, 0).astype(np.float32), np.float32([0, 3.0, 6.0]), np.float32(0.9),
                np.float32([1, 1, 0]))
-    img, st = _slab_chain(data, es, bounds, lights, r.VolumeIllumination, ra_args, W, H, shade)
+    img, st = _slab_chain(data, es, bounds, lights, r.VolumeIllumination, ra_args, W, H, merged)
     assert full.max() > 0
     assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
     assert not st[4].any()  # every ray finished
+    if shade == "exact" and lanes == "1":
+        S = O.OracleSession()
+        oh = S.new()
+        ov = O.OVolume(data, 3)
+        S.sync_volumes(oh, 0, ov, O.OVolume(np.ones((1, 1), np.float32), 5), ov)
+        olut = O.OVolume(r.VolumeIllumination.Data, 7)
+        oargs = [np.asarray(a) for a in ra_args]
+        olights = np.array([[500, 1000, 550, 0, 1, 1], [0, 550, 90, 1, 0.5, 1]], np.float32)
+        ref32, _ = S.render(oh, olights, olut, *oargs, threads=4)
+        ref64, _ = S.render(oh, olights, olut, *oargs, double=True, threads=4)
+        assert_parity(img, ref32, ref64, f"slab chain {case}")
     r.delete()
+
+
+def test_slab_render_checks_the_bound_planes(counter_clock):
+    """vr_render_slab reads the BOUND emission volume (the last sync on any handle, as vr_render
+    does); a slab whose bound planes would reach past the volume depth is refused, not marched
+    (its virtual plane base would address memory outside the resident buffer)."""
+    import torch
+    from volume_renderer_amd import mex
+    W, H = 32, 24
+    lights = [vr.LightSource([500, 1000, 550], [0, 1, 1])]
+    ra, keep = mex.render_args(lights, vr.Volume(vr.HenyeyGreenstein(16)), np.float32([1.0, 0.4, 0.6]),
+                               np.float32([1, 1, 1]), np.uint64([H, W]), np.flip(O.rotation(125, 25, 0), 0).astype(np.float32),
+                               np.float32([0, 3.0, 6.0]), np.float32(0.9), np.float32([1, 1, 0]))
+    state = torch.zeros(mex.SLAB_PLANES * W * H, dtype=torch.float32, device="cuda")
+    h = vr.volumeRender("new")
+    big = vr.Volume(O.shell_volume(40)[:, :, :30].copy(order="F"))
+    vr.volumeRender("sync_volumes", h, np.uint64(0), big, vr.Volume(1), big)
+    with pytest.raises(Exception):
+        mex.render_slab(h, ra, mex.slab(40, 20, 20.0, np.inf, +1), 0, state.data_ptr())
+    mex.render_slab(h, ra, mex.slab(40, 10, 12.0, np.inf, +1), 0, state.data_ptr())  # planes 10..39: fits
+    torch.cuda.synchronize()
+    vr.volumeRender("delete", h)
 
 
 @pytest.mark.parametrize("lit", [True, False])

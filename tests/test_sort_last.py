@@ -1,9 +1,12 @@
 """Sort-last slab protocol on CPU: world_size 2 and 3 over gloo.
 
 A stand-in for vr_render_slab with the same contract (per-ray state: premultiplied colour, alpha,
-"goes on"; a slab composites only the samples it owns, in ray order, and stops a ray at sum.a >
-thr) checks the pipelined two-sweep hand-off of volume_renderer_amd.parallel: the result must
-equal compositing every ray's samples in one process, bit for bit.  The kernel itself is checked
+"goes on", and the resume point -- here the index of the ray's next sample; a slab composites
+only the samples it owns, in ray order, stops a ray at sum.a > thr, and hands it off at its first
+sample beyond the slab; direction 0 marches both kinds of ray) checks the pipelined two-sweep
+hand-off of volume_renderer_amd.parallel: the result must equal compositing every ray's samples
+in one process, bit for bit, and no slab may replay a sample before it (every ray resumes where
+the previous slab stopped).  The kernel itself is checked
 against the one-volume render on the GPU (test_gpu_parity.py::test_sort_last_slabs_...)."""
 import os
 import socket
@@ -66,43 +69,54 @@ def _worker(rank, world, port, q):
         z, dz, c, a = _rays()
         z0, z1 = parallel.slab_bounds(int(DEPTH), world)[rank]
 
+        replayed = [0]
+
         def render_tile(t, direction, fresh, buf):  # stand-in for vr_render_slab on tile t
-            st = buf.numpy().reshape(3, -1)            # planes: colour, alpha, goes-on
+            st = buf.numpy().reshape(4, -1)            # planes: colour, alpha, goes-on, resume index
             for j, i in enumerate(_tile_rays(t)):
-                if (dz[i] >= 0) != (direction > 0):
+                if direction != 0 and (dz[i] >= 0) != (direction > 0):
                     if fresh:
-                        st[:, j] = (0, 0, 1)
+                        st[:, j] = (0, 0, 1, 0)
                     continue
                 s = np.zeros(2, np.float32) if fresh else st[:2, j].copy()
                 go = True if fresh else st[2, j] != 0
+                k = 0 if fresh else int(st[3, j])      # resume at the next sample
                 past = False
-                for k in range(NSAMP if go else 0):
+                while go and k < NSAMP:
                     zk = z[i, k]
                     if not (z0 <= zk < z1):
                         if (zk >= z1) if dz[i] >= 0 else (zk < z0):
                             past = True
                             break
+                        replayed[0] += 1               # before the slab
+                        k += 1
                         continue
-                    if _composite(s, c[i, k], a[i, k]):
+                    stop = _composite(s, c[i, k], a[i, k])
+                    k += 1
+                    if stop:
                         break
                 st[:2, j] = s
                 st[2, j] = 1.0 if past else 0.0
+                st[3, j] = k
 
-        states = [torch.zeros(3 * len(_tile_rays(t))) for t in range(NTILES)]
+        states = [torch.zeros(4 * len(_tile_rays(t))) for t in range(NTILES)]
         parallel.sort_last_sweeps(render_tile, states, world, rank)
         if rank == 0:
             out = np.zeros((NRAY, 2), np.float32)
             for t in range(NTILES):
-                st = states[t].numpy().reshape(3, -1)
+                st = states[t].numpy().reshape(4, -1)
                 out[_tile_rays(t)] = st[:2].T
                 assert not st[2].any()
-            q.put(out)
+            q.put((out, replayed[0]))
+        else:
+            assert replayed[0] == 0
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_pipelined_slab_sweeps_equal_one_volume(world):
+    """world 1: one process renders each tile once (direction 0, both kinds of ray)."""
     ref = _reference()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -110,11 +124,12 @@ def test_pipelined_slab_sweeps_equal_one_volume(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got, replayed = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert replayed == 0  # every slab resumed at the ray's next sample: nothing replayed
 
 
 def test_slab_bounds_partition_the_depth():

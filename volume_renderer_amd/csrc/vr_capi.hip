@@ -711,6 +711,59 @@ int depth_lanes(const vr::RenderParams &P) {
 // fusable (optional, vr_render_channels): a frame the multi-view march can take (staged march,
 // gradient mode 0/1, 32-bit addressing) is only prepared -- F.P complete, *fusable = 1, nothing
 // launched; any other frame is rendered here as usual and *fusable = 0.
+// Longest-first schedule: a frame of the same shape as an earlier one launches its workgroups in
+// the order of that frame's measured block durations, so the long tiles start first instead of
+// forming the tail (the image is the same for any order).  VR_SCHED=0: off.  Only for short
+// launches (< VR_SCHED_ROUNDS K = 1 waves per device wave slot): with many rounds the tail is a
+// small part of the frame and the row-major order keeps neighbouring tiles (which share voxels in
+// L2) running together (metric frame: 43.6 ms row-major, 45.0 ms sorted).
+bool want_schedule(const vr::RenderParams &P) {
+  const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) / device_wave_slots();
+  return P.views < 2 && (env_flag("VR_SCHED") || (!env_flag_off("VR_SCHED") && rounds < VR_SCHED_ROUNDS));
+}
+
+// Attach the schedule of this launch shape (`extra` tells launches of one shape apart, e.g. the
+// slab and sweep of a sort-last launch) to P: wg_order / wg_cost / sched_blocks / prio_blocks.
+hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, const Frame &F, int K, hipStream_t stream,
+                           const char *extra) {
+  typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
+  static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
+                                    vr::fast::march_blocks_k8};
+  const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
+  const uint32_t nb = bfns[ki](P);
+  // keyed by stream too: the order buffer of one stream is never rewritten under another's launch
+  char key[300];
+  std::snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%d/%u/%p/%s", K, P.width, P.height, P.part, P.num_parts,
+                P.block_cols, F.mode, P.wide_slot, P.fast_shade, nb, (void *)stream, extra);
+  vr_context::Schedule &S = h->sched[key];
+  if (!S.d_cost && nb) {
+    if (hipMalloc(&S.d_cost, nb * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&S.d_order, nb * sizeof(uint32_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      if (S.d_cost) (void)hipFree(S.d_cost);
+      S.d_cost = nullptr;
+      S.d_order = nullptr;
+    }
+    S.blocks = nb;
+  }
+  if (!(S.d_cost && S.blocks == nb)) return hipSuccess;
+  hipError_t rc;
+  if (S.measured) {
+    rc = vr::launch_order(S.d_cost, nb, S.d_order, stream);
+  } else {  // first launch of this shape: row-major order, durations recorded
+    rc = vr::launch_iota(S.d_order, nb, stream);
+    S.measured = true;
+  }
+  if (rc != hipSuccess) return rc;
+  P.wg_order = S.d_order;
+  P.wg_cost = S.d_cost;
+  P.sched_blocks = nb;
+  // the first round of workgroups (the longest ones) at raised wave priority (A/B: VR_PRIO_BLOCKS)
+  P.prio_blocks = (uint32_t)(device_wave_slots() / 4);
+  if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
+  return hipSuccess;
+}
+
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
               unsigned long long *d_steps, hipStream_t stream, Frame &F, float *d_out2 = nullptr,
               const float *eye2 = nullptr, int *fusable = nullptr) {
@@ -817,48 +870,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
         {vr::exact::launch_march_k1, vr::exact::launch_march_k2, vr::exact::launch_march_k4, vr::exact::launch_march_k8},
         {vr::fast::launch_march_k1, vr::fast::launch_march_k2, vr::fast::launch_march_k4, vr::fast::launch_march_k8}};
     const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
-    // Longest-first schedule: a frame of the same shape as an earlier one launches its
-    // workgroups in the order of that frame's measured block durations, so the long tiles start
-    // first instead of forming the tail (the image is the same for any order).  VR_SCHED=0: off.
-    // Only for short launches (< VR_SCHED_ROUNDS K = 1 waves per device wave slot): with many rounds
-    // the tail is a small part of the frame and the row-major order keeps neighbouring tiles (which
-    // share voxels in L2) running together (metric frame: 43.6 ms row-major, 45.0 ms sorted).
-    const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) / device_wave_slots();
-    const bool sched = P.views < 2 && (env_flag("VR_SCHED") || (!env_flag_off("VR_SCHED") && rounds < VR_SCHED_ROUNDS));
-    if (!P.steps && sched && K > 1) {
-      static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
-                                        vr::fast::march_blocks_k4, vr::fast::march_blocks_k8};
-      const uint32_t nb = bfns[ki](P);
-      // keyed by stream too: the order buffer of one stream is never rewritten under another's launch
-      char key[200];
-      std::snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%d/%u/%p", K, P.width, P.height, P.part, P.num_parts,
-                    P.block_cols, F.mode, P.wide_slot, P.fast_shade, nb, (void *)stream);
-      vr_context::Schedule &S = h->sched[key];
-      if (!S.d_cost && nb) {
-        if (hipMalloc(&S.d_cost, nb * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(&S.d_order, nb * sizeof(uint32_t)) != hipSuccess) {
-          (void)hipGetLastError();
-          if (S.d_cost) (void)hipFree(S.d_cost);
-          S.d_cost = nullptr;
-          S.d_order = nullptr;
-        }
-        S.blocks = nb;
-      }
-      if (S.d_cost && S.blocks == nb) {
-        if (S.measured) {
-          VR_HIP(vr::launch_order(S.d_cost, nb, S.d_order, stream));
-        } else {  // first launch of this shape: row-major order, durations recorded
-          VR_HIP(vr::launch_iota(S.d_order, nb, stream));
-          S.measured = true;
-        }
-        P.wg_order = S.d_order;
-        P.wg_cost = S.d_cost;
-        P.sched_blocks = nb;
-        // the first round of workgroups (the longest ones) at raised wave priority (A/B: VR_PRIO_BLOCKS)
-        P.prio_blocks = (uint32_t)(device_wave_slots() / 4);
-        if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
-      }
-    }
+    if (!P.steps && K > 1 && want_schedule(P)) VR_HIP(attach_schedule(h, P, F, K, stream, ""));
     if (P.views > 1) {
       static const blocks_fn vfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
                                         vr::fast::march_blocks_k4, vr::fast::march_blocks_k8};
@@ -896,8 +908,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
 int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, const vr_partition *part,
                    const float *d_in, float *d_out, hipStream_t stream, Frame &F) {
   if (!sl || !d_out) return fail(VR_ERR_ARGUMENT, "slab / output is NULL");
-  const VolRec &ev = h->vol[T_EM];
-  if (sl->depth == 0 || sl->z_first + ev.dims[2] > sl->depth || (sl->direction != 1 && sl->direction != -1))
+  if (sl->depth == 0 || sl->z_first >= sl->depth || (sl->direction < -1 || sl->direction > 1))
     return fail(VR_ERR_ARGUMENT, "invalid slab");
   if (a->num_lights > 0 && !a->lights) return fail(VR_ERR_ARGUMENT, "lights is NULL");
   upload_lights(h, a);
@@ -905,6 +916,10 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   if (rc) return rc;
   vr::RenderParams &P = F.P;
   if (F.degenerate || !P.em.p || P.em.one) return fail(VR_ERR_UNSUPPORTED, "slab render needs a synced emission volume");
+  // the planes resident are those of the BOUND emission texture (the last sync_volumes of any
+  // handle, as every render reads -- render.cpp binds globally); the slab must lie inside them
+  const uint64_t res_nz = (uint64_t)P.em.nz, res_nx = (uint64_t)P.em.nx;
+  if (sl->z_first + res_nz > sl->depth) return fail(VR_ERR_ARGUMENT, "invalid slab: bound planes exceed the depth");
   if (F.mode == 2 || !F.ab_alias) return fail(VR_ERR_UNSUPPORTED, "slab render: lookup gradients / separate absorption");
   // the resident planes addressed by their global padded index: virtual base z_first planes back
   const bool re_em = P.re_is_em != 0;
@@ -917,7 +932,7 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   // resident padded planes holding the right data: the synced planes, plus the edge-replicating
   // apron planes only at the ends of the whole volume
   P.slab_pk0 = (int32_t)(sl->z_first + (sl->z_first > 0 ? 1 : 0));
-  P.slab_pk1 = (int32_t)(sl->z_first + ev.dims[2] + 1 + (sl->z_first + ev.dims[2] == sl->depth ? 1 : 0));
+  P.slab_pk1 = (int32_t)(sl->z_first + res_nz + 1 + (sl->z_first + res_nz == sl->depth ? 1 : 0));
   const double D = (double)sl->depth;
   P.slab_z0 = std::isfinite(sl->z0) ? (float)(sl->z0 / D) : -INFINITY;
   P.slab_z1 = std::isfinite(sl->z1) ? (float)(sl->z1 / D) : INFINITY;
@@ -929,8 +944,6 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
     P.tap_off[2] = (float)((F.mode == 1 ? (double)P.gstep[2] * P.bscale[2] * D : 0.0) + 0.0625);
     P.tap_half = half_texel_taps(P, F.mode, (float)D);  // judged on the whole volume, as one render
   }
-  set_chunk_halo(F, 4);  // the slab launch marches with up to 4 depth lanes (chunks <= 64 samples)
-  P.slab_margin = P.tap_off[2] / P.em.fnz;  // bound of the chunk ownership test, normalized
   P.slab_dir = sl->direction;
   P.slab_in = d_in;
   rc = validate_partition(part);
@@ -939,17 +952,21 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   P.part = part ? part->part : 0;
   P.num_parts = part ? part->num_parts : 1;
   P.part_cols = (int32_t)part_columns(P.width, P.block_cols, P.part, P.num_parts);
-  P.plane_cols = P.part_cols;  // the state of a part is dense: five [part_cols][H] planes
+  P.plane_cols = P.part_cols;  // the state of a part is dense: VR_SLAB_PLANES [part_cols][H] planes
+  if ((uint64_t)P.part_cols * (uint64_t)P.height >= (1ull << 32))
+    return fail(VR_ERR_UNSUPPORTED, "slab render: more than 2^32 rays in one part");
   P.out = d_out;
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
   {
     const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
-    const double tau = (f > 0 && P.width > 0) ? dist * (double)ev.dims[0] / ((double)P.width * f) : 1e30;
+    const double tau = (f > 0 && P.width > 0) ? dist * (double)res_nx / ((double)P.width * f) : 1e30;
     P.wide_slot = tau > 1.5 ? 1 : 0;
   }
   // depth lanes as for the one-volume march (a tile of a pipelined sweep is a short launch)
   int K = depth_lanes(P);
   if (K > 4) K = 4;
+  set_chunk_halo(F, K);
+  P.slab_margin = P.tap_off[2] / P.em.fnz;  // bound of the chunk ownership test, normalized
   typedef hipError_t (*slab_fn)(const vr::RenderParams &, int, hipStream_t);
   static const slab_fn sfns[2][3] = {
       {vr::exact::launch_march_slab_k1, vr::exact::launch_march_slab_k2, vr::exact::launch_march_slab_k4},
@@ -959,6 +976,12 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   L.device = h->device;
   bind_reads(L);
   stage_frame(L, P, g_tex.lights);
+  if (K > 1 && want_schedule(P)) {  // a tile of a sweep is a short launch: longest-first schedule
+    char extra[120];
+    std::snprintf(extra, sizeof extra, "slab/%llu/%llu/%g/%g/%d", (unsigned long long)sl->depth,
+                  (unsigned long long)sl->z_first, sl->z0, sl->z1, sl->direction);
+    VR_HIP(attach_schedule(h, P, F, K, stream, extra));
+  }
   VR_HIP(sfns[P.fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](P, F.mode, stream));
   VR_HIP(L.finish());
   return VR_OK;

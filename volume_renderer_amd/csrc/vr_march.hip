@@ -86,6 +86,37 @@ struct Ray {
   bool past;  // slab mode: the ray left this rank's slab still unfinished (the next slab goes on)
 };
 
+// Slab mode: the ray's resume point -- the recurrence state (t, pos, sample index) of its next
+// sample, the first one this slab does not own -- goes straight to the state planes 5-9 of P.out
+// at pixel index kk (registers are the march's limit; a ray hands off once).
+__device__ __forceinline__ void store_resume(const RenderParams &P, uint32_t kk, float t, const f3 &pos, int32_t n) {
+  const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
+  P.out[kk + 5 * plane] = t;
+  P.out[kk + 6 * plane] = pos.x;
+  P.out[kk + 7 * plane] = pos.y;
+  P.out[kk + 8 * plane] = pos.z;
+  P.out[kk + 9 * plane] = __int_as_float(n);
+}
+
+// K > 1, called by whole groups: (t, p, n) = (t0, p0, n0) of the first lane (in sample order) of
+// this lane's group with flagf != 0, in every lane of the group (I descending: the lowest flagged
+// lane writes last).
+template <int K, int I = K - 1>
+__device__ __forceinline__ void first_of_group(float flagf, float t0, const f3 &p0, int32_t n0, float &t, f3 &p,
+                                               int32_t &n) {
+  if constexpr (I >= 0) {
+    const float x = group_lane<K, I>(p0.x), y = group_lane<K, I>(p0.y), z = group_lane<K, I>(p0.z);
+    const float tt = group_lane<K, I>(t0);
+    const int32_t nn = __float_as_int(group_lane<K, I>(__int_as_float(n0)));
+    if (group_lane<K, I>(flagf) != 0.f) {
+      t = tt;
+      p = mk(x, y, z);
+      n = nn;
+    }
+    first_of_group<K, I - 1>(flagf, t0, p0, n0, t, p, n);
+  }
+}
+
 struct ChunkStats {
   uint32_t staged, leap, fall, iter, lit;
 };
@@ -281,23 +312,25 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // takes its sample, then every lane composites the group's samples in order; `alive` (the ray:
 // not stopped by sum.a > thr and some sample left) is the same in all K lanes.  Bit-identical to
 // K = 1; samples after an early exit are computed and discarded.
-// SLAB (sort-last bricks; K = 1 only): the emission texture holds planes of one
-// z-slab of a larger volume, and only the samples this slab owns (slab_z0 <= p.z < slab_z1 in
-// normalized coordinates) are fetched and composited; the others replay the march recurrences
-// only, so every owned sample has the position, t and step count of the one-volume march.  A ray
-// stops here when it leaves the slab in its direction of travel (`past`), or terminates.
+// SLAB (sort-last bricks): the emission texture holds planes of one z-slab of a
+// larger volume, and only the samples this slab owns (slab_z0 <= p.z < slab_z1 in normalized
+// coordinates) are fetched and composited.  A ray arrives with the recurrence state of its next
+// sample (the resume point the previous slab handed off, or its start); samples before the slab
+// (only when a sweep does not begin at an end slab) replay the recurrences, so every owned sample
+// has the position, t and step count of the one-volume march.  A ray stops here when it
+// terminates, or at its first sample beyond the slab in its direction of travel (`past`), whose
+// state becomes the resume point (store_resume).
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
-__device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C) {
+__device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
+                                      uint32_t kk = 0) {
   static_assert(!COUNT || K == 1, "the counter variant is built for K = 1 only");
   static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
   const float sbz = P.bmin[2], ssz = P.bscale[2];
-  const bool asc = R.step.z >= 0.f;  // slab order along this ray
   // slab mode: the ray has left the slab in its direction of travel (normalized z of its sample)
-  auto beyond = [&](float zn) { return asc ? zn >= P.slab_z1 : zn < P.slab_z0; };
+  auto beyond = [&](float zn) { return R.step.z >= 0.f ? zn >= P.slab_z1 : zn < P.slab_z0; };
   const DevTex &E = P.em;
   const int sub = lane & (K - 1);
-  if constexpr (K > 1) {
-    R.nsteps = 0;
+  if constexpr (K > 1) {  // R.nsteps: 0, or the resume point's index (slab mode)
     R.mine = R.alive;
     leap(P, sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to this lane's first sample
     R.alive = group_any<K>(R.mine);
@@ -311,38 +344,25 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     int box_vol = 0;
     plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B,
                     COUNT ? &box_vol : nullptr);
+    bool inside = true;  // slab mode: every sample of this chunk lies in the slab
     if constexpr (SLAB) {
-      // a chunk none of whose samples this slab owns only replays the recurrences
-      bool own = false;
+      // a chunk none of whose samples this slab owns is not staged: its samples only replay the
+      // recurrences (before the slab) or hand the ray off at the first one beyond it, sample by
+      // sample, so the resume point is exact
+      bool own = false, in = true;
       if (R.alive) {
         const float zs = (R.pos.z - sbz) * ssz;
         const float ze = (fmaf(R.step.z, (float)(S - 1), R.pos.z) - sbz) * ssz;
         own = fmaxf(zs, ze) + P.slab_margin >= P.slab_z0 && fminf(zs, ze) - P.slab_margin < P.slab_z1;
+        in = fminf(zs, ze) - P.slab_margin >= P.slab_z0 && fmaxf(zs, ze) + P.slab_margin < P.slab_z1;
       }
-      if (!__any(own)) {
-        if constexpr (K == 1) {
-          advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
-          if (R.alive && beyond((R.pos.z - sbz) * ssz)) {
-            R.alive = false;
-            R.past = true;
-          }
-        } else {
-          advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
-          R.alive = R.alive && group_any<K>(R.mine);
-          // the ray's next sample is lane 0's
-          const bool b0 = group_lane<K, 0>(beyond((R.pos.z - sbz) * ssz) ? 1.f : 0.f) != 0.f;
-          if (R.alive && b0) {
-            R.alive = false;
-            R.past = true;
-          }
-        }
-        continue;
-      }
+      if (!__any(own)) staged = false;
+      inside = __all(in);  // every sample of the chunk is owned: no per-sample test
       // only this slab's planes are resident: clamp the staged box to them (the owned samples'
       // taps lie inside; the others are not fetched)
       const int z_lo = max(B.rz, P.slab_pk0), z_hi = min(B.rz + B.ez, P.slab_pk1);
       if (staged) {
-        if (z_hi <= z_lo) {
+        if (z_hi - z_lo < 3) {  // (the half-texel tap test assumes boxes of >= 3 planes)
           staged = false;
         } else {
           B.rz = z_lo;
@@ -359,7 +379,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       const bool nonzero = stage_box<BIG>(L, E, B, lane);  // always stage: the samples read the slot
       // leap only when the absorption texture is the staged one: a zero emission box says nothing
       // about the opacity of a separate absorption texture (the simEmAb slot path)
-      empty = AB_ALIAS && P.skip_empty && !partial && !nonzero;
+      // slab mode: only a chunk wholly inside the slab (a leap must not carry a ray past its hand-off
+      // sample: the samples beyond are the next slab's, and its data is not in this box)
+      empty = AB_ALIAS && P.skip_empty && !partial && !nonzero && (!SLAB || inside);
     }
     __builtin_amdgcn_wave_barrier();
     if (COUNT) ++(staged && !partial ? (empty ? C.leap : C.staged) : C.fall);
@@ -378,10 +400,11 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     // ---- S samples ---------------------------------------------------------------------------
     if constexpr (K == 1) {
       for (int k = 0; k < S && R.alive; ++k) {
-        if constexpr (SLAB) {
+        if (SLAB && !inside) {
           const float zn = (R.pos.z - sbz) * ssz;  // the sampler's own p.z
           if (!(zn >= P.slab_z0 && zn < P.slab_z1)) {
-            if (beyond(zn)) {
+            if (beyond(zn)) {  // this sample is the next slab's first
+              store_resume(P, kk, R.t, R.pos, R.nsteps);
               R.alive = false;
               R.past = true;
             } else {  // before the slab: the recurrences of one sample (composite without colour)
@@ -411,7 +434,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       for (int k = 0; k < S && R.alive; k += K) {
         float r = 0.f, gg = 0.f, b = 0.f, alpha = 0.f;
         bool ex = R.mine, take = R.mine;
-        if constexpr (SLAB) {
+        if (SLAB && !inside) {
           // a sample beyond the slab ends the ray here (beyond is monotone along the ray, so the
           // group's existing samples stay a prefix); one before it adds exactly nothing (colour 0,
           // opacity 0: the sums and the exit test are unchanged)
@@ -424,8 +447,15 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
         }
         composite_group<K, 0>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
-        if constexpr (SLAB) {
+        if (SLAB && !inside) {
           if (R.alive && group_any<K>(R.mine && !ex)) {  // left the slab still unfinished
+            // the next slab resumes at the group's first sample beyond this one (samples of a
+            // group are in lane order: the first flagged lane of the group stores it)
+            float t = R.t;
+            f3 p = R.pos;
+            int32_t n = R.nsteps;
+            first_of_group<K>((R.mine && !ex) ? 1.f : 0.f, R.t, R.pos, R.nsteps, t, p, n);
+            if (sub == 0) store_resume(P, kk, t, p, n);  // one store per pixel, from lane 0 as the others
             R.alive = false;
             R.past = true;
           }
@@ -652,17 +682,30 @@ hipError_t VR_CAT(launch_march_views_k, VR_MARCH_K)(const RenderViews &V, uint32
 }
 
 // Sort-last slab launch: one wave per 8x8 tile of the image part (the columns of
-// the image partition, vr_partition); per pixel the ray state (premultiplied r, g, b, alpha, and
-// 1 if the ray goes on past this slab) is read from P.slab_in (null: a fresh ray), marched
-// through this slab's samples and written to P.out as five [plane_cols][H] planes.  Rays whose direction does not match the sweep (P.slab_dir: +1 = rays with
-// dir.z >= 0 in ascending slab order, -1 = dir.z < 0 descending) pass their state through.
-template <int K, int MODE, int CAP>
-__global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const RenderParams P) {
+// the image partition, vr_partition); per pixel the ray state is read from P.slab_in (null: a
+// fresh ray), marched through this slab's samples and written to P.out as VR_SLAB_PLANES
+// [plane_cols][H] planes: premultiplied r, g, b, alpha; 1 if the ray goes on past this slab; and
+// the resume point of a ray that goes on -- t, pos.x, pos.y, pos.z and the sample index (int32
+// bits) of its next sample -- so the next slab continues the recurrences where this one stopped
+// instead of replaying them from the ray start.  Rays whose direction does not match the sweep
+// (P.slab_dir: +1 = rays with dir.z >= 0 in ascending slab order, -1 = dir.z < 0 descending; 0 =
+// both, for the top slab, where the descending rays start) pass their state through (a fresh ray's
+// resume point is its start).
+// SH / SCHED as for march_kernel: the half-texel tap launch; the longest-first schedule.
+#ifndef VR_SLAB_MIN_EU
+#define VR_SLAB_MIN_EU VR_MARCH_MIN_EU
+#endif
+template <int K, int MODE, bool SH, int CAP, bool SCHED>
+__global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= 1664 && !SCHED) ? VR_SLAB_MIN_EU : 1) void march_slab_kernel(
+    const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
-  const int tile = (int)blockIdx.x * VR_WG_WAVES + wave;
+  const uint64_t clk0 = SCHED ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint32_t wg = SCHED ? P.wg_order[blockIdx.x] : blockIdx.x;
+  if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
+  const int tile = (int)wg * VR_WG_WAVES + wave;
   const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
   const int blk = tile >> 2, quad = tile & 3;
   const int ray = lane >> TS::LK;
@@ -672,7 +715,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const Rend
   const int pb = lc / P.block_cols;
   const int x = (P.part + pb * P.num_parts) * P.block_cols + (lc - pb * P.block_cols);
   const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
-  const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
+  const uint32_t kk = (uint32_t)lc * (uint32_t)P.height + (uint32_t)y;  // plane < 2^32 (host check)
   Ray R;
   R.o = mk(0.f, 0.f, 0.f);
   R.pos = R.o;
@@ -687,28 +730,42 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const Rend
   bool go_on = true;  // the incoming state: the ray has not terminated
   ChunkStats C{0, 0, 0, 0, 0};
   if (active) {
-    if (P.slab_in) {
-      R.sr = P.slab_in[kk];
-      R.sg = P.slab_in[kk + plane];
-      R.sb = P.slab_in[kk + 2 * plane];
-      R.sa = P.slab_in[kk + 3 * plane];
-      go_on = P.slab_in[kk + 4 * plane] != 0.f;
-    }
     f3 d;
     float tnear;
     const bool hit = ray_setup(P, x, y, R.o, d, tnear, R.tfar);
     R.pos = mk(fmaf(d.x, tnear, R.o.x), fmaf(d.y, tnear, R.o.y), fmaf(d.z, tnear, R.o.z));
     R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
     R.t = tnear;
-    const bool mine_dir = (P.slab_dir > 0) == (R.step.z >= 0.f);
+    if (P.slab_in) {
+      R.sr = P.slab_in[kk];
+      R.sg = P.slab_in[kk + plane];
+      R.sb = P.slab_in[kk + 2 * plane];
+      R.sa = P.slab_in[kk + 3 * plane];
+      go_on = P.slab_in[kk + 4 * plane] != 0.f;
+      if (go_on) {  // resume at the next sample
+        R.t = P.slab_in[kk + 5 * plane];
+        R.pos = mk(P.slab_in[kk + 6 * plane], P.slab_in[kk + 7 * plane], P.slab_in[kk + 8 * plane]);
+        R.nsteps = __float_as_int(P.slab_in[kk + 9 * plane]);
+      }
+    }
+    const bool mine_dir = P.slab_dir == 0 || (P.slab_dir > 0) == (R.step.z >= 0.f);
     R.alive = hit && go_on && mine_dir;
     R.past = go_on && !mine_dir;  // another sweep's ray: passed through unchanged
     if (!hit) R.past = false;
   }
+  // the resume point as it stands (a ray passed through keeps it; one handed off below replaces it)
+  if (active && (lane & (K - 1)) == 0) store_resume(P, kk, R.t, R.pos, R.nsteps);
   if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<K, MODE, true, false, false, true, false, CAP, true>(P, L, lane, R, C);
+    march<K, MODE, true, false, SH, true, false, CAP, true>(P, L, lane, R, C, kk);
   else
-    march<K, MODE, true, false, false, true, true, CAP, true>(P, L, lane, R, C);
+    march<K, MODE, true, false, SH, true, true, CAP, true>(P, L, lane, R, C, kk);
+  if (SCHED) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
+      P.wg_cost[wg] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+    }
+  }
   if (active && (lane & (K - 1)) == 0) {
     P.out[kk] = R.sr;
     P.out[kk + plane] = R.sg;
@@ -720,6 +777,20 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES) void march_slab_kernel(const Rend
 
 // Host entry of the slab launch (launch_march_slab_k1 / _k2 / _k4): MODE 0 or 1, absorption
 // aliasing emission, the emission texture addressed with 64-bit offsets from its virtual base.
+template <int MODE, bool SH, int CAP>
+static void launch_slab_c(const RenderParams &P, dim3 grid, hipStream_t s) {
+  constexpr int K = VR_MARCH_K;
+  const dim3 blk(64 * VR_WG_WAVES);
+  if (P.wg_order) hipLaunchKernelGGL((march_slab_kernel<K, MODE, SH, CAP, true>), grid, blk, 0, s, P);
+  else hipLaunchKernelGGL((march_slab_kernel<K, MODE, SH, CAP, false>), grid, blk, 0, s, P);
+}
+
+template <int MODE, bool SH>
+static void launch_slab_m(const RenderParams &P, dim3 grid, hipStream_t s) {
+  if (P.wide_slot) launch_slab_c<MODE, SH, VR_LDS_CAP_WIDE>(P, grid, s);
+  else launch_slab_c<MODE, SH, VR_LDS_CAP>(P, grid, s);
+}
+
 hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mode, hipStream_t s) {
   constexpr int K = VR_MARCH_K;
   using TS = TileShape<K>;
@@ -727,14 +798,11 @@ hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mo
   if (mode > 1) return hipErrorInvalidValue;
   const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
-  const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES)), blk(64 * VR_WG_WAVES);
-  if (mode == 0) {
-    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<K, 0, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_slab_kernel<K, 0, VR_LDS_CAP>), grid, blk, 0, s, P);
-  } else {
-    if (P.wide_slot) hipLaunchKernelGGL((march_slab_kernel<K, 1, VR_LDS_CAP_WIDE>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_slab_kernel<K, 1, VR_LDS_CAP>), grid, blk, 0, s, P);
-  }
+  const dim3 grid((unsigned)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES));
+  if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || K == 1)) return hipErrorInvalidValue;
+  if (mode == 0) launch_slab_m<0, false>(P, grid, s);
+  else if (VR_MARCH_FAST && P.tap_half) launch_slab_m<1, true>(P, grid, s);
+  else launch_slab_m<1, false>(P, grid, s);
   return hipGetLastError();
 }
 #endif

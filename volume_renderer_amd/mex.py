@@ -175,9 +175,13 @@ def partition_columns(width: int, part) -> int:
     return int(lib().vr_partition_columns(int(width), ctypes.byref(part) if part is not None else None))
 
 
+SLAB_PLANES = 10  # include/vrhip.h VR_SLAB_PLANES
+
+
 def slab(depth: int, z_first: int, z0: float, z1: float, direction: int) -> _lib.VrSlab:
     """vr_slab: the synced emission volume holds planes [z_first, ...) of a volume of depth
-    `depth`; the render owns the samples with z0 <= p.z * depth < z1; direction +1 / -1."""
+    `depth`; the render owns the samples with z0 <= p.z * depth < z1; direction +1 / -1, or 0
+    (both: the top slab's ascending launch, where the descending rays start)."""
     s = _lib.VrSlab()
     s.depth, s.z_first, s.z0, s.z1, s.direction = int(depth), int(z_first), float(z0), float(z1), int(direction)
     return s
@@ -195,7 +199,8 @@ def slab_planes(dims, element_size_um, z0: float, z1: float):
 def render_slab(handle, ra: VrRenderArgs, sl, d_state_in: int, d_state_out: int, stream: int = 0,
                 part=None) -> None:
     """vr_render_slab: march this slab's samples of every ray (of the part's columns, if a
-    partition is given); state = 5 planes of cols*H floats."""
+    partition is given); state = SLAB_PLANES planes of cols*H floats (colour, alpha, goes-on,
+    and the resume point t, x, y, z, sample index of a ray that goes on)."""
     check(lib().vr_render_slab(_handle(handle), ctypes.byref(ra), ctypes.byref(sl),
                                ctypes.byref(part) if part is not None else None,
                                ctypes.c_void_p(int(d_state_in)) if d_state_in else None,

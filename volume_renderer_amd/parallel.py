@@ -41,12 +41,15 @@ def gather_partitions(local, gathered, world: int, rank: int, group=None) -> Non
 # ---- sort-last z-slabs -----------------------------------------
 # Volumes larger than one GPU: rank r holds only the planes of z-slab r (vr_slab_planes) and
 # marches only the samples that slab owns (vr_render_slab).  A ray's samples are composited in ray
-# order by handing the exact ray state (premultiplied rgb, alpha, "goes on") from slab to slab:
-# rays with dir.z >= 0 visit the slabs in ascending z (rank 0 -> world-1), the others descending
-# (world-1 -> 0).  The image is cut into `ntiles` column tiles (vr_partition parts) so that the
-# ranks work on different tiles at the same time: rank r renders tile t of the ascending sweep once
-# rank r-1 has sent it, then the descending sweep runs back down; rank 0 ends with every ray's
-# final state, bit-identical to the one-volume render.
+# order by handing the exact ray state (premultiplied rgb, alpha, "goes on", and the resume point:
+# t, position and sample index of its next sample) from slab to slab: rays with dir.z >= 0 visit
+# the slabs in ascending z (rank 0 -> world-1), the others descending (world-1 -> 0), each slab
+# continuing the march where the previous one stopped.  The descending rays start in the top slab,
+# so the last rank marches both kinds in one launch (direction 0) and the descending sweep proper
+# runs over ranks world-2 .. 0.  The image is cut into `ntiles` column tiles (vr_partition parts)
+# so that the ranks work on different tiles at the same time: rank r renders tile t of the
+# ascending sweep once rank r-1 has sent it, then the descending sweep runs back down; rank 0 ends
+# with every ray's final state, bit-identical to the one-volume render.
 
 def slab_bounds(depth: int, world: int):
     """Owned ranges [z0, z1) of `world` equal z-slabs of a depth-`depth` volume (the end slabs
@@ -56,29 +59,46 @@ def slab_bounds(depth: int, world: int):
             for r in range(world)]
 
 
-def sort_last_sweeps(render_tile, states, world: int, rank: int, group=None) -> None:
+def sort_last_sweeps(render_tile, states, world: int, rank: int, group=None, streams=None) -> None:
     """Run the two pipelined sweeps.  `render_tile(t, direction, fresh, buf)` renders this rank's
-    slab for tile t in place on buf (fresh: the tile's rays start here, no incoming state);
-    `states[t]` is this rank's state buffer of tile t (a tensor the backend can send).  On return
-    rank 0's buffers hold the final state of every tile."""
+    slab for tile t in place on buf (direction +1 / -1, or 0 = both on the top slab; fresh: the
+    tile's rays start here, no incoming state) on the current stream; `states[t]` is this rank's
+    state buffer of tile t (a tensor the backend can send).  On return rank 0's buffers hold the
+    final state of every tile.  One process (world 1) renders each tile once, both directions.
+    streams (optional, device tensors): tile t's receive, render and send run on streams[t % n], so
+    that consecutive tiles' launches overlap their tails; the current stream waits for them all."""
+    import contextlib
+
+    import torch
     import torch.distributed as dist
+    last = rank == world - 1
+    on = (lambda t: torch.cuda.stream(streams[t % len(streams)])) if streams else (lambda t: contextlib.nullcontext())
+    if streams:
+        for s in streams:  # the buffers and the volume were produced on the current stream
+            s.wait_stream(torch.cuda.current_stream())
     pending = []
-    # ascending sweep: rank 0 starts every tile fresh
+    # ascending sweep: rank 0 starts every tile fresh; the top slab also starts the descending rays
     for t, buf in enumerate(states):
-        if rank > 0:
-            dist.recv(buf, src=rank - 1, group=group)
-        render_tile(t, +1, rank == 0, buf)
-        if rank < world - 1:
-            pending.append(dist.isend(buf, dst=rank + 1, group=group))
+        with on(t):
+            if rank > 0:
+                dist.recv(buf, src=rank - 1, group=group)
+            render_tile(t, 0 if last else +1, rank == 0, buf)
+            if not last:
+                pending.append(dist.isend(buf, dst=rank + 1, group=group))
     for w in pending:
         w.wait()
     pending = []
-    # descending sweep: the last rank continues from its own ascending result
+    # descending sweep: the top slab hands its tiles down (sent only now, so that every pair of
+    # ranks sees its messages in one order: the ascending ones first)
     for t, buf in enumerate(states):
-        if rank < world - 1:
-            dist.recv(buf, src=rank + 1, group=group)
-        render_tile(t, -1, False, buf)
-        if rank > 0:
-            pending.append(dist.isend(buf, dst=rank - 1, group=group))
+        with on(t):
+            if not last:
+                dist.recv(buf, src=rank + 1, group=group)
+                render_tile(t, -1, False, buf)
+            if rank > 0:
+                pending.append(dist.isend(buf, dst=rank - 1, group=group))
     for w in pending:
         w.wait()
+    if streams:
+        for s in streams:
+            torch.cuda.current_stream().wait_stream(s)
