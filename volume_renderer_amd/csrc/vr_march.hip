@@ -184,8 +184,9 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
                      (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2))) {
       // every shading lane's taps lie in the staged box (the tap cells a - 1 .. a + 1 per axis,
       // a = i + hi): the taps from the slot with their shared voxels and partial sums
-      const f3 d = half_grad_lds(L, B, ac, sx, sy, sz, ax.w, ay.w, az.w, C);
-      g = mk(d.x * 0.5f, d.y * 0.5f, d.z * 0.5f);
+      // unhalved: the fast shading uses g only through n = -g * rsq(g.g), which the exact factor 2
+      // leaves bit-identical (4x scales g.g by a power of two; rsq halves exactly)
+      g = half_grad_lds(L, B, ac, sx, sy, sz, ax.w, ay.w, az.w, C);
     } else if (HALF_TAPS && (HALF_ONLY || P.tap_half)) {
       // fast variant, gradient offset of exactly half a texel on every axis (a power-of-two cube,
       // vr_capi.hip half_texel_taps): each axis' two taps derived from the centre's (half_taps);
@@ -207,8 +208,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
       l = lz + (sz.hi ? 1 : 0);
       a = ac + (sz.hi ? B.pxy : 0);
       g.z = fetch_at<BIG>(E, L, B, sxy && in_box(l, B.ez), a, ax, ay, p) -
-            fetch_at<BIG>(E, L, B, sxy && in_box(l - 1, B.ez), a - B.pxy, ax, ay, m);
-      g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
+            fetch_at<BIG>(E, L, B, sxy && in_box(l - 1, B.ez), a - B.pxy, ax, ay, m);  // unhalved, as above
     } else if (MODE == 1) {  // computeGradient on tex_emission (gem == em), world offsets +-gstep
       const float xp = ((pos.x + P.gstep[0]) - bmin.x) * bsc.x;
       const float xm = ((pos.x - P.gstep[0]) - bmin.x) * bsc.x;

@@ -155,9 +155,10 @@ struct AxF {
 // that is NaN or rounds past +-1).  One v_med3 does the NaN -> 0 substitution (the median of NaN,
 // 0 and 1 is min3 = 0 under the hardware's NaN rule) and keeps c in [0, 1], where the floor of
 // c*n - 0.5 is already in [-1, n-1]: the same axis as axis_f, without its compare, select and clamp.
+template <bool FMA = false>
 __device__ __forceinline__ AxF axis_lut(float c, float fn) {
   c = __builtin_amdgcn_fmed3f(c, 0.f, 1.f);
-  const float xb = c * fn - 0.5f;
+  const float xb = FMA ? fmaf(c, fn, -0.5f) : c * fn - 0.5f;  // FMA: the fast variant's shading
   const float fl = floorf(xb);
   const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
   return AxF{fl, w};
@@ -180,16 +181,44 @@ __device__ __forceinline__ float fetch_small(const DevTex &t, const AxF &ax, con
   const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
   return lerp(c0, c1, az.w);
 }
+// Two fetch_small lookups sharing the x axis, all eight row loads issued before the first lerp.
+__device__ __forceinline__ void fetch_small2(const DevTex &t, const AxF &ax, const AxF &ay0, const AxF &az0,
+                                             const AxF &ay1, const AxF &az1, float &v0, float &v1) {
+  const float ox = fmaf(ax.fl, 4.f, t.fbase4);
+  const uint32_t o0 = (uint32_t)fmaf(az0.fl, t.fpxy4, fmaf(ay0.fl, t.fpx4, ox));
+  const uint32_t o1 = (uint32_t)fmaf(az1.fl, t.fpxy4, fmaf(ay1.fl, t.fpx4, ox));
+  const uint32_t px4 = t.px * 4u, pxy4 = t.pxy * 4u;
+  const char *b = reinterpret_cast<const char *>(t.p);
+  const f2a4 a00 = *reinterpret_cast<const f2a4 *>(b + o0);
+  const f2a4 a10 = *reinterpret_cast<const f2a4 *>(b + (o0 + px4));
+  const f2a4 a01 = *reinterpret_cast<const f2a4 *>(b + (o0 + pxy4));
+  const f2a4 a11 = *reinterpret_cast<const f2a4 *>(b + (o0 + pxy4 + px4));
+  const f2a4 b00 = *reinterpret_cast<const f2a4 *>(b + o1);
+  const f2a4 b10 = *reinterpret_cast<const f2a4 *>(b + (o1 + px4));
+  const f2a4 b01 = *reinterpret_cast<const f2a4 *>(b + (o1 + pxy4));
+  const f2a4 b11 = *reinterpret_cast<const f2a4 *>(b + (o1 + pxy4 + px4));
+  {
+    const float c00 = lerp(a00.x, a00.y, ax.w), c10 = lerp(a10.x, a10.y, ax.w);
+    const float c01 = lerp(a01.x, a01.y, ax.w), c11 = lerp(a11.x, a11.y, ax.w);
+    v0 = lerp(lerp(c00, c10, ay0.w), lerp(c01, c11, ay0.w), az0.w);
+  }
+  {
+    const float c00 = lerp(b00.x, b00.y, ax.w), c10 = lerp(b10.x, b10.y, ax.w);
+    const float c01 = lerp(b01.x, b01.y, ax.w), c11 = lerp(b11.x, b11.y, ax.w);
+    v1 = lerp(lerp(c00, c10, ay1.w), lerp(c01, c11, ay1.w), az1.w);
+  }
+}
 __device__ __forceinline__ Ax to_ax(const AxF &a) { return Ax{(int)a.fl, a.w}; }
 
 // The LUT value of one light (0 if the illumination texture is unbound).
+template <bool FMA = false>
 __device__ __forceinline__ float lut_light(const DevTex &lut, const AxF &la, float beta, float gamma) {
   if (lut.p == nullptr) return 0.f;
   if (lut.one) {
     const float q = lut.p[0];
     return fmaf(0.5f, q - q, q);
   }
-  const AxF lb = axis_lut(beta, lut.fny), lg = axis_lut(gamma, lut.fnz);
+  const AxF lb = axis_lut<FMA>(beta, lut.fny), lg = axis_lut<FMA>(gamma, lut.fnz);
   if (lut.small) return fetch_small(lut, la, lb, lg);
   return fetch<false>(lut, to_ax(la), to_ax(lb), to_ax(lg));
 }
@@ -346,9 +375,37 @@ __device__ __forceinline__ float divpi(float x) {
   return fmaf(fmaf(-q, VR_PI, x), r, q);
 }
 
-// acos(q) / pi in one rounding (device library acospi) for the fast shading variant
+// acos(q) / pi for the fast shading variant.  VR_FAST_ACOS 0: the device library's acospi (one
+// rounding, ~21 VALU); 1: acospi(t) = sqrt(1 - t) * P8(t) on t = |q| (the form of Abramowitz &
+// Stegun 4.4.46; P8 a weighted least-squares fit at Chebyshev nodes of acos(t) / (pi sqrt(1 - t)),
+// relative approximation error 2.4e-9), acospi(q) = 1 - acospi(-q) for q < 0: 13 VALU.  In fp32,
+// over every q in [-1, 1]: 94 % correctly rounded, at most 1.95 ulp.  NaN and |q| > 1 give NaN as
+// acosf does (sqrt of a negative).
+#ifndef VR_FAST_ACOS
+#define VR_FAST_ACOS 1
+#endif
+#ifndef VR_FAST_NLEN
+#define VR_FAST_NLEN 1  // 1: the fast variant takes the unit normal's length as 1 (shade_lights)
+#endif
 extern "C" __device__ float __ocml_acospi_f32(float);
-__device__ __forceinline__ float acospi_q(float q) { return __ocml_acospi_f32(q); }
+__device__ __forceinline__ float acospi_q(float q) {
+#if VR_FAST_ACOS
+  const float t = fabsf(q);
+  float p = 2.209365193e-04f;
+  p = fmaf(p, t, -1.277460018e-03f);
+  p = fmaf(p, t, 3.530717921e-03f);
+  p = fmaf(p, t, -6.615247577e-03f);
+  p = fmaf(p, t, 1.037604921e-02f);
+  p = fmaf(p, t, -1.610660180e-02f);
+  p = fmaf(p, t, 2.833945118e-02f);
+  p = fmaf(p, t, -6.830968708e-02f);
+  p = fmaf(p, t, 0.5f);
+  const float r = __builtin_amdgcn_sqrtf(1.f - t) * p;
+  return q < 0.f ? 1.f - r : r;
+#else
+  return __ocml_acospi_f32(q);
+#endif
+}
 
 // 1 - __expf(-a * dx) (volumeRender_kernel.cu:456).  Exact variant: the correctly rounded-ish
 // device expf the oracle models; fast variant: what __expf is, exp2 of x * log2(e) on the
@@ -378,13 +435,19 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
     const float dli = dot3(li, n);
     const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-    const float rn = __builtin_amdgcn_rsqf(dot3(n, n)), rlip = __builtin_amdgcn_rsqf(dot3(lip, lip));
+    // |n| is 1 to within the rsq's ulp: its length is not divided out again (VR_FAST_NLEN 0 does)
+#if VR_FAST_NLEN
+    const float rn = 1.f;
+#else
+    const float rn = __builtin_amdgcn_rsqf(dot3(n, n));
+#endif
+    const float rlip = __builtin_amdgcn_rsqf(dot3(lip, lip));
     const float alpha_n = acospi_q(dot3(n, li) * (rn * __builtin_amdgcn_rsqf(dot3(li, li))));
-    const AxF la = axis_lut(alpha_n, P.lut.fnx);
+    const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
     int i = 0;
     if (P.lut.p != nullptr && P.lut.small && !P.lut.one) {
       // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
-      // lights, so that a pair's eight LUT row loads issue together, ahead of their lerps
+      // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
       for (; i + 1 < P.num_lights; i += 2) {
         const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
         const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
@@ -396,8 +459,9 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
         const float gamma0 = acospi_q(dot3(lip, lop0) * (rlip * __builtin_amdgcn_rsqf(dot3(lop0, lop0))));
         const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
         const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
-        const float light0 = fetch_small(P.lut, la, axis_lut(beta0, P.lut.fny), axis_lut(gamma0, P.lut.fnz));
-        const float light1 = fetch_small(P.lut, la, axis_lut(beta1, P.lut.fny), axis_lut(gamma1, P.lut.fnz));
+        float light0, light1;
+        fetch_small2(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
+                     axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
         const float rl0 = refl * light0;
         ir = fmaf(rl0 * L0.cr, P.color[0], ir);
         ig = fmaf(rl0 * L0.cg, P.color[1], ig);
@@ -419,8 +483,8 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       const float gamma0 = acospi_q(dot3(lip, lop0) * (rlip * __builtin_amdgcn_rsqf(dot3(lop0, lop0))));
       const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
       const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
-      const float light0 = lut_light(P.lut, la, beta0, gamma0);
-      const float light1 = lut_light(P.lut, la, beta1, gamma1);
+      const float light0 = lut_light<true>(P.lut, la, beta0, gamma0);
+      const float light1 = lut_light<true>(P.lut, la, beta1, gamma1);
       const float rl0 = refl * light0;
       ir = fmaf(rl0 * L0.cr, P.color[0], ir);
       ig = fmaf(rl0 * L0.cg, P.color[1], ig);
@@ -437,7 +501,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
       const float beta = acospi_q(dlo * (rn * __builtin_amdgcn_rsqf(dot3(lo, lo))));
       const float gamma = acospi_q(dot3(lip, lop) * (rlip * __builtin_amdgcn_rsqf(dot3(lop, lop))));
-      const float rl = refl * lut_light(P.lut, la, beta, gamma);
+      const float rl = refl * lut_light<true>(P.lut, la, beta, gamma);
       ir = fmaf(rl * L.cr, P.color[0], ir);
       ig = fmaf(rl * L.cg, P.color[1], ig);
       ib = fmaf(rl * L.cb, P.color[2], ib);

@@ -54,7 +54,9 @@ __device__ __forceinline__ int wave_min(int v) { return wave_reduce<false>(v); }
 __device__ __forceinline__ int wave_max(int v) { return wave_reduce<true>(v); }
 
 #ifndef VR_ODD_PITCH
-#define VR_ODD_PITCH 0   // 1: odd LDS row / plane pitches (measured slower: larger slots overflow more)
+// LDS row / plane pitches: 0 dense (ex, ex * ey); 1 always odd (measured slower: the larger slots
+// overflow more); 2 odd when the padded box still fits the slot, dense otherwise
+#define VR_ODD_PITCH 0
 #endif
 
 // Staged box: padded-volume index ranges [r0, r0 + e) per axis, stored in the slot with row
@@ -214,7 +216,7 @@ __device__ __forceinline__ bool stage_box_elems(float *L, const DevTex &t, const
 template <bool BIG>
 __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &B, int lane) {
   const int ex = B.ex, ey = B.ey;
-  if (ex > 64 || B.pxy != B.px * ey) return stage_box_elems(L, t, B, lane);
+  if (ex > 64) return stage_box_elems(L, t, B, lane);
   if (!BIG && (uint64_t)t.pxy * (uint64_t)B.ez * 4u >= 0xFFFFFFFFull)  // 32-bit byte offsets overflow
     return stage_box_elems(L, t, B, lane);
   typedef typename std::conditional<BIG, uint64_t, uint32_t>::type off_t;
@@ -229,8 +231,9 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
   off_t g = ((off_t)z * t.pxy + (off_t)y * t.px + (off_t)xr) * 4u;               // bytes
   const off_t g_row = (off_t)per * t.px * 4u;
   const off_t g_wrap = ((off_t)t.pxy - (off_t)ey * t.px) * 4u;
-  int l = rr * B.px + xr;  // slot word (pxy == px * ey: row r starts at r * px)
+  int l = z * B.pxy + y * B.px + xr;  // slot word
   const int l_row = per * B.px;
+  const int l_wrap = B.pxy - ey * B.px;  // plane padding (0 for dense pitches)
   uint32_t acc = 0;
   for (int k0 = 0; k0 < n; k0 += VR_STAGE_UNROLL) {
     float v[VR_STAGE_UNROLL];
@@ -245,6 +248,7 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
       while (y >= ey) {
         y -= ey;
         g += g_wrap;
+        l += l_wrap;
       }
     }
 #pragma unroll
@@ -300,11 +304,18 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
     B.ex = wave_max(hi[0]) - B.rx + 1;
     B.ey = wave_max(hi[1]) - B.ry + 1;
     B.ez = wave_max(hi[2]) - B.rz + 1;
-    B.px = VR_ODD_PITCH ? (B.ex | 1) : B.ex;
-    B.pxy = VR_ODD_PITCH ? ((B.px * B.ey) | 1) : B.px * B.ey;
+    B.px = VR_ODD_PITCH == 1 ? (B.ex | 1) : B.ex;
+    B.pxy = VR_ODD_PITCH == 1 ? ((B.px * B.ey) | 1) : B.px * B.ey;
     if (vol_out) *vol_out = B.pxy * B.ez;
     if (B.ex <= 0 || B.ey <= 0 || B.ez <= 0) return;  // no live ray
     if (B.pxy * B.ez <= CAP) {
+      if (VR_ODD_PITCH == 2) {  // rows and planes on rotating banks, if the slot has room
+        const int px = B.ex | 1, pxy = (px * B.ey) | 1;
+        if (pxy * B.ez <= CAP) {
+          B.px = px;
+          B.pxy = pxy;
+        }
+      }
       staged = true;
       return;
     }
