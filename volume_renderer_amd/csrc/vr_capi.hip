@@ -485,6 +485,24 @@ struct Frame {
 };
 
 
+// Per-sample bound of the drift between a predicted position fma(step, k, pos) and k sequentially
+// rounded additions, in emission texels per axis: |pos| <= |box| + |eye| (fp32 rounding 1.2e-7 per
+// operation, two per step).  eye2: the second eye of a fused stereo launch, whose rays start
+// elsewhere (the bound must cover both eyes).
+void drift_bound(Frame &F, const float *eye2) {
+  const vr::RenderParams &P = F.P;
+  double pmax = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    double e = std::fabs(P.eye[i]);
+    if (eye2) e = std::max(e, (double)std::fabs(eye2[i]));
+    pmax = std::max(pmax, (double)std::fabs(P.bmin[i]) + e);
+  }
+  for (int i = 0; i < 3; ++i) {
+    const float n = i == 0 ? P.em.fnx : (i == 1 ? P.em.fny : P.em.fnz);
+    F.drift1[i] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[i] * (double)n;
+  }
+}
+
 int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth_override = 0) {
   vr::RenderParams &P = F.P;
   std::memset(&P, 0, sizeof(P));
@@ -560,11 +578,9 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
   // position fma(step, k, pos) and k sequentially rounded additions (|pos| <= |box| + |eye|), per
   // sample of the chunk; set_chunk_halo scales it by the launch's chunk length
   {
-    double pmax = 0.0;
-    for (int i = 0; i < 3; ++i) pmax = std::max(pmax, (double)std::fabs(P.bmin[i]) + std::fabs(P.eye[i]));
+    drift_bound(F, nullptr);
     for (int i = 0; i < 3; ++i) {
       const float n = i == 0 ? P.em.fnx : (i == 1 ? P.em.fny : P.em.fnz);
-      F.drift1[i] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[i] * (double)n;
       P.tap_off[i] = (float)((F.mode == 1 ? (double)P.gstep[i] * P.bscale[i] * n : 0.0) + 0.0625);
     }
     P.tap_half = half_texel_taps(P, F.mode, P.em.fnz);
@@ -813,6 +829,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     P.views = 2;
     P.out2 = d_out2;
     for (int i = 0; i < 3; ++i) P.eye2[i] = eye2[i];
+    drift_bound(F, eye2);  // the staging halo covers the second eye's rays too
   }
   if (F.degenerate) {
     if (out_bytes) VR_HIP(hipMemsetAsync(d_out, 0, out_bytes, stream));
