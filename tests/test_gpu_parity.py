@@ -703,3 +703,38 @@ def test_channels_device_images_and_fp32_sum(counter_clock):
     assert np.array_equal(s.cpu().numpy().view(np.uint32), want.view(np.uint32))
     for r in hr + dr:
         r.delete()
+
+
+def test_scheduled_partition_under_a_changing_camera(monkeypatch, counter_clock):
+    """The longest-first schedule of a short partitioned launch (one part of 8, depth lanes, few
+    waves per wave slot) orders workgroups by the PREVIOUS launch of the same shape; under a camera
+    that moves every frame that order is stale.  The image must not depend on it: every frame of
+    the scheduled part equals the same part rendered unscheduled (VR_SCHED=0), bit for bit."""
+    import torch
+    from volume_renderer_amd import mex
+    n, W, H = 64, 320, 200
+    v = vr.Volume(O.shell_volume(n))
+    lut = vr.Volume(vr.HenyeyGreenstein(32))
+    lights = [vr.LightSource([500, 1000, 550], [0, 1, 1]), vr.LightSource([0, 550, 90], [1, 0.5, 1])]
+    h = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h, np.uint64(0), v, vr.Volume(1), v)
+    part = mex.partition(16, 3, 8)
+    cols = mex.partition_columns(W, part)
+    assert mex.depth_lanes(cols, H) > 1
+    out = torch.empty(3 * cols * H, dtype=torch.float32, device="cuda")
+    for k in range(6):
+        R = np.flip(O.rotation(125 + 9 * k, 25 - 4 * k, 3 * k), 0).astype(np.float32)
+        ra, keep = mex.render_args(lights, lut, np.float32([1, 0.4, 0.6]), np.float32([1, 1, 1]),
+                                   np.uint64([H, W]), R, np.float32([0, 3, 6]), np.float32(0.9), np.float32([1, 1, 0]))
+        monkeypatch.delenv("VR_SCHED", raising=False)
+        mex.render_device(h, ra, out.data_ptr(), part)
+        torch.cuda.synchronize()
+        sched = out.cpu().numpy().copy()
+        monkeypatch.setenv("VR_SCHED", "0")
+        mex.render_device(h, ra, out.data_ptr(), part)
+        torch.cuda.synchronize()
+        plain = out.cpu().numpy()
+        assert plain.max() > 0
+        assert np.array_equal(sched.view(np.uint32), plain.view(np.uint32)), k
+    monkeypatch.delenv("VR_SCHED", raising=False)
+    vr.volumeRender("delete", h)
