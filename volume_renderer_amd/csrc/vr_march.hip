@@ -494,7 +494,11 @@ template <int K>
 struct TileShape {
   static constexpr int LR = (K == 1 ? 6 : K == 2 ? 5 : K == 4 ? 4 : 3);  // log2 rays per wave
   static constexpr int LK = 6 - LR;                                         // log2 K
-  static constexpr int TW = 1 << (LR / 2), TH = 1 << (LR - LR / 2);       // tile width, height
+#ifndef VR_TILE_WLOG
+#define VR_TILE_WLOG -1  // log2 tile width override (A/B; -1: square-ish, the taller for odd LR)
+#endif
+  static constexpr int LW = (VR_TILE_WLOG >= 0 && VR_TILE_WLOG <= LR) ? VR_TILE_WLOG : LR / 2;
+  static constexpr int TW = 1 << LW, TH = 1 << (LR - LW);  // tile width, height
 };
 
 // SCHED: the launch follows P.wg_order and records each block's duration in P.wg_cost (a
