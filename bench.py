@@ -275,7 +275,7 @@ def main():
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else ""),
-                       "depth_lanes": mex.depth_lanes(my_cols, H),
+                       "depth_lanes": mex.depth_lanes(my_cols, H, 6.0 * n / (W * 3.0)),  # dist * n / (W * f)
                        "frames": "serial, one HIP stream"},
             "samples_per_frame": total_samples,
             "shaded_samples_per_frame": total_lit,

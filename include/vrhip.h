@@ -225,9 +225,13 @@ int vr_slab_planes(const uint64_t dims[3], const float element_size_um[3], doubl
                    uint64_t *count);
 
 /* Depth lanes (lanes per ray) the march kernel uses for a launch of part_cols x
- * height rays on the current device: 1, 2, 4 or 8 (VR_DEPTH_LANES overrides).  Launches with few
- * waves per wave slot of the device also follow a longest-first workgroup schedule. */
+ * height rays on the current device at about one texel per pixel: 1, 2, 4 or 8 (VR_DEPTH_LANES
+ * overrides).  A render also weighs the texels its pixels span (denser sampling: more lanes).
+ * Launches with few waves per wave slot of the device also follow a longest-first schedule. */
 int vr_depth_lanes(int64_t part_cols, int64_t height);
+/* The same for a render whose pixels span `texels_per_pixel` texels at the volume
+ * (dist * d0 / (W * f) for the reference's camera). */
+int vr_depth_lanes_tau(int64_t part_cols, int64_t height, double texels_per_pixel);
 
 /* Synthetic test volume V_shell(n) of SURVEY.md 8d, generated on the device into d_out[n^3]. */
 int vr_synth_shell_device(float *d_out, uint64_t n, void *stream);

@@ -82,6 +82,7 @@ SIGNATURES = [
     ("vr_assemble_partitions", c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int64, c_void_p,
                                        c_void_p]),
     ("vr_depth_lanes", c_int, [c_int64, c_int64]),
+    ("vr_depth_lanes_tau", c_int, [c_int64, c_int64, ctypes.c_double]),
     ("vr_render_slab", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrSlab), POINTER(VrPartition), c_void_p,
                                 c_void_p, c_void_p]),
     ("vr_slab_planes", c_int, [POINTER(c_uint64), POINTER(c_float), ctypes.c_double, ctypes.c_double,

@@ -73,10 +73,16 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 }  // namespace vr
 
 #ifndef VR_DEPTH_ROUNDS_K1
-#define VR_DEPTH_ROUNDS_K1 16.0  // K = 1 at >= this many K = 1 waves per device wave slot (tuned on MI355X)
+#define VR_DEPTH_ROUNDS_K1 16.0  // K = 1 needs >= this many K = 1 waves per device wave slot (and sparse sampling)
 #endif
 #ifndef VR_DEPTH_ROUNDS_K2
 #define VR_DEPTH_ROUNDS_K2 3.0   // K = 2 at >= this many, K = 4 below
+#endif
+#ifndef VR_DEPTH_TAU_K4
+#define VR_DEPTH_TAU_K4 1.5      // K = 4 from this many texels per pixel (depth_lanes)
+#endif
+#ifndef VR_DEPTH_TAU_K1
+#define VR_DEPTH_TAU_K1 0.5      // K = 1 (with >= VR_DEPTH_ROUNDS_K1 rounds) below this many
 #endif
 
 #ifndef VR_SCHED_ROUNDS
@@ -711,6 +717,13 @@ int device_wave_slots() {
   return slots;
 }
 
+// Depth lanes of a launch from its length (K = 1 waves per device wave slot) and the texels a pixel
+// spans (P.tau; 0 = unknown, taken as 1).  Few rounds: K = 4 shortens the tail.  Otherwise the
+// staged box -- the hull of a wave's ray bundle over a chunk -- decides: its lateral extent grows
+// with tau and with the tile (64 / K rays), and a hull that overflows the slot halves the chunk and
+// restages.  Measured on MI355X (ms): tau 2.0 (C2, 1024x768, 3 rounds) K = 4 19.5, K = 2 29.8,
+// K = 8 25.1; tau 1.07 (metric, 7.9 rounds) K = 2 36.5, K = 4 37.6, K = 1 51.7; tau 1.0 (C5,
+// 4096^2, 64 rounds) K = 2 293.6, K = 4 338.5, K = 1 348.7.  K = 1 only for sparse sampling.
 int depth_lanes(const vr::RenderParams &P) {
   if (const char *ev = std::getenv("VR_DEPTH_LANES")) {
     const int k = std::atoi(ev);
@@ -718,7 +731,24 @@ int depth_lanes(const vr::RenderParams &P) {
   }
   const double waves = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0);  // at K = 1
   const double rounds = waves / device_wave_slots();
-  return rounds >= VR_DEPTH_ROUNDS_K1 ? 1 : rounds >= VR_DEPTH_ROUNDS_K2 ? 2 : 4;
+  const double tau = P.tau > 0.f ? (double)P.tau : 1.0;
+  if (rounds < VR_DEPTH_ROUNDS_K2 || tau >= VR_DEPTH_TAU_K4) return 4;
+  if (rounds >= VR_DEPTH_ROUNDS_K1 && tau < VR_DEPTH_TAU_K1) return 1;
+  return 2;
+}
+
+// texels a pixel spans at the volume, tau = dist * vw / (W * f) (pixel pitch 2/W on the image plane
+// at f, box x-extent 2 = vw texels), and the wave slot size it asks for at the launch's depth lanes:
+// 12 KiB slots once the hull of a 4x8 tile (K <= 2) passes tau 1.5 (tau 2.0: 18 % faster than
+// 6.5 KiB), of a 4x4 tile (K = 4) tau 3 (tau 2.0 at K = 4: 19.5 ms with 6.5 KiB slots, 20.7 with
+// 12 KiB).  VR_WIDE_SLOT=0/1 overrides (A/B).
+void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
+  const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
+  const double tau = (f > 0 && P.width > 0) ? dist * vw / ((double)P.width * f) : 1e30;
+  P.tau = (float)std::min(tau, 1e30);
+  const int K = P.steps ? 1 : depth_lanes(P);
+  P.wide_slot = tau > (K >= 4 ? 3.0 : 1.5) ? 1 : 0;
+  if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
 }
 
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
@@ -809,17 +839,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   P.out = d_out;
   P.steps = d_steps;
   P.tile_mode = 0;
-  // wave slot size of the march: the 8x8-ray footprint per chunk grows with the texels a pixel
-  // spans at the volume, tau = dist * vw / (W * f) (pixel pitch 2/W on the image plane at f, box
-  // x-extent 2 = vw texels).  Measured: tau 1.07 (1920 px) is fastest with small slots, tau 2.0
-  // (1024 px) 18 % faster with 12 KiB ones.  VR_WIDE_SLOT=0/1 overrides (A/B).
-  {
-    const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
-    const double vw = (double)h->vol[T_EM].dims[0];
-    const double tau = (f > 0 && P.width > 0) ? dist * vw / ((double)P.width * f) : 1e30;
-    P.wide_slot = tau > 1.5 ? 1 : 0;
-    if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
-  }
+  set_tau_and_slot(P, a, (double)h->vol[T_EM].dims[0]);  // depth lanes and wave slot size
   // shading arithmetic: hardware rsq / exp2 by default; VR_EXACT_SHADE=1 selects
   // the oracle's correctly rounded op sequence (bit-identical to oracle/vr_oracle.c up to acosf)
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
@@ -974,11 +994,8 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
     return fail(VR_ERR_UNSUPPORTED, "slab render: more than 2^32 rays in one part");
   P.out = d_out;
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
-  {
-    const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
-    const double tau = (f > 0 && P.width > 0) ? dist * (double)res_nx / ((double)P.width * f) : 1e30;
-    P.wide_slot = tau > 1.5 ? 1 : 0;
-  }
+  P.steps = nullptr;
+  set_tau_and_slot(P, a, (double)res_nx);
   // depth lanes as for the one-volume march (a tile of a pipelined sweep is a short launch)
   int K = depth_lanes(P);
   if (K > 4) K = 4;
@@ -1684,6 +1701,15 @@ int vr_depth_lanes(int64_t part_cols, int64_t height) {
   std::memset(&P, 0, sizeof(P));
   P.part_cols = (int32_t)std::min<int64_t>(part_cols, 0x7fffffff);
   P.height = (int32_t)std::min<int64_t>(height, 0x7fffffff);
+  return depth_lanes(P);
+}
+
+int vr_depth_lanes_tau(int64_t part_cols, int64_t height, double texels_per_pixel) {
+  vr::RenderParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.part_cols = (int32_t)std::min<int64_t>(part_cols, 0x7fffffff);
+  P.height = (int32_t)std::min<int64_t>(height, 0x7fffffff);
+  P.tau = (float)texels_per_pixel;
   return depth_lanes(P);
 }
 

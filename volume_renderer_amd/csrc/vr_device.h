@@ -59,6 +59,7 @@ struct RenderParams {
   const float *gvec;              // lookup gradient interleaved (gx,gy,gz,0) x padded voxels, or null
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
+  float tau;                      // host only: texels a pixel spans at the volume (depth_lanes)
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)
   int32_t wide_slot;              // march: 12 KiB wave slots instead of 6 KiB (vr_stage.h)
   int32_t fast_shade;             // 1: hardware-rsq shading and exp2 opacity (default); 0: the oracle's ops

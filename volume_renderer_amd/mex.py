@@ -207,9 +207,12 @@ def render_slab(handle, ra: VrRenderArgs, sl, d_state_in: int, d_state_out: int,
                                ctypes.c_void_p(int(d_state_out)), ctypes.c_void_p(int(stream))))
 
 
-def depth_lanes(part_cols: int, height: int) -> int:
-    """Depth lanes the march uses for a launch of this shape on the current device (vr_depth_lanes)."""
-    return int(lib().vr_depth_lanes(int(part_cols), int(height)))
+def depth_lanes(part_cols: int, height: int, texels_per_pixel=None) -> int:
+    """Depth lanes the march uses for a launch of this shape on the current device (vr_depth_lanes;
+    with texels_per_pixel, vr_depth_lanes_tau: the choice a render at that sampling density makes)."""
+    if texels_per_pixel is None:
+        return int(lib().vr_depth_lanes(int(part_cols), int(height)))
+    return int(lib().vr_depth_lanes_tau(int(part_cols), int(height), float(texels_per_pixel)))
 
 
 def render_device(handle, ra: VrRenderArgs, d_out: int, part=None, d_steps: int = 0, stream: int = 0) -> None:
