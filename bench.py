@@ -76,6 +76,8 @@ def main():
                          "the device with vr_gradient_device")
     ap.add_argument("--lights", type=int, default=2, help="light sources (0: emission-absorption only; "
                     "diagnostics, the metric config has 2)")
+    ap.add_argument("--rotate", type=float, nargs=3, default=[125.0, 25.0, 0.0],
+                    help="camera rotate(alpha, beta, gamma) (metric config: 125 25 0; others are diagnostics)")
     ap.add_argument("--sim-parts", type=int, default=0,
                     help="diagnostic (1 GPU): also time each rank's share of a P-way column partition, "
                          "the kernel time a rank would see at --gpus P")
@@ -125,7 +127,7 @@ def main():
         vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em, *gvols)
     else:
         vr.volumeRender("sync_volumes", h, np.uint64(0), em, refl, em)  # Em, Re, Ab (Ab aliases Em)
-    R = rotation(125, 25, 0)
+    R = rotation(*args.rotate)
     ra, keep = mex.render_args(lights, lut, np.float32([1.0, 0.4, 0.6]), np.float32([1, 1, 1]),
                                np.uint64([H, W]), np.flip(R, 0).astype(np.float32), np.float32([0, 3.0, 6.0]),
                                np.float32(0.9), np.float32([1, 1, 0]))
@@ -271,7 +273,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic V_shell(%d) (SURVEY.md 8d), generated in HBM" % n,
-            "config": {"workload": workload_name(n, W, H, L, args.gradient),
+            "config": {"workload": workload_name(n, W, H, L, args.gradient)
+                       + ("" if list(args.rotate) == [125.0, 25.0, 0.0]
+                          else " [diagnostic camera rotate(%g,%g,%g)]" % tuple(args.rotate)),
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else ""),

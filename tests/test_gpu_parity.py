@@ -738,3 +738,32 @@ def test_scheduled_partition_under_a_changing_camera(monkeypatch, counter_clock)
         assert np.array_equal(sched.view(np.uint32), plain.view(np.uint32)), k
     monkeypatch.delenv("VR_SCHED", raising=False)
     vr.volumeRender("delete", h)
+
+
+@pytest.mark.parametrize("tail_pct", ["0", "60"])
+def test_full_frame_schedule_keeps_the_image(monkeypatch, counter_clock, tail_pct):
+    """Full frames (many waves per wave slot) are measured on their first launch and every
+    VR_SCHED_REMEASURE-th after; when the heaviest block would form a tail the frames follow the
+    heavy-first order (VR_SCHED_TAIL_PCT=0 forces it), else no schedule.  Whatever the order, every
+    frame equals the unscheduled render bit for bit, through measured, ordered and re-measured
+    launches under a moving camera."""
+    monkeypatch.setenv("VR_SCHED_TAIL_PCT", tail_pct)
+    monkeypatch.setenv("VR_SCHED_REMEASURE", "3")
+    v = vr.Volume(O.shell_volume(64))
+    frames = {}
+    for mode in ("sched", "plain"):
+        if mode == "plain":
+            monkeypatch.setenv("VR_SCHED_FULL", "0")
+        else:
+            monkeypatch.delenv("VR_SCHED_FULL", raising=False)
+        r = ex1_renderer(v, res=(1280, 1280))
+        out = []
+        for k in range(7):
+            r.rotate(4 if k else 0, 2 if k else 0, 0)
+            out.append(r.render())
+        frames[mode] = out
+        r.delete()
+    monkeypatch.delenv("VR_SCHED_FULL", raising=False)
+    for k, (a, b) in enumerate(zip(frames["sched"], frames["plain"])):
+        assert a.max() > 0
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k

@@ -49,8 +49,8 @@ def mean(kpattern, counter):
     return sum(xs) / len(xs) if xs else None
 
 
-# metric config: march_kernel<K, MODE 1, absorption aliases emission, no counters, half-texel launch or not, 32-bit, slot, unscheduled>
-march = r"march_kernel<\d, 1, true, false, (?:true|false), false, \d+, false>"
+# metric config: march_kernel<K, MODE 1, absorption aliases emission, no counters, half-texel launch or not, 32-bit, slot, unscheduled or full-frame schedule>
+march = r"march_kernel<\d, 1, true, false, (?:true|false), false, \d+, (?:false|0|2)>"
 fetch_kb, write_kb = mean(march, "FETCH_SIZE"), mean(march, "WRITE_SIZE")
 if fetch_kb is not None:
     traffic = 2 * 1024 * fetch_kb + 1024 * (write_kb or 0.0)

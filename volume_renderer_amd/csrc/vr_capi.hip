@@ -54,7 +54,8 @@ hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool bi
 VR_DECL_MARCH(fast)
 VR_DECL_MARCH(exact)
 #undef VR_DECL_MARCH
-hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s);
+hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s, uint32_t heavy_div,
+                        uint64_t tail);
 hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
@@ -77,6 +78,15 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 #endif
 #ifndef VR_DEPTH_ROUNDS_K2
 #define VR_DEPTH_ROUNDS_K2 3.0   // K = 2 at >= this many, K = 4 below
+#endif
+#ifndef VR_SCHED_HEAVY_DIV
+#define VR_SCHED_HEAVY_DIV 8  // full-frame schedule: heavy = duration >= the longest block's / this
+#endif
+#ifndef VR_SCHED_TAIL_PCT
+#define VR_SCHED_TAIL_PCT 60  // heavy-first only when the longest block >= this % of the packed frame
+#endif
+#ifndef VR_SCHED_REMEASURE
+#define VR_SCHED_REMEASURE 16  // full frames: block durations re-measured every this many launches
 #endif
 #ifndef VR_DEPTH_TAU_K4
 #define VR_DEPTH_TAU_K4 1.5      // K = 4 from this many texels per pixel (depth_lanes)
@@ -177,6 +187,13 @@ struct vr_context {
     uint32_t *d_cost = nullptr, *d_order = nullptr;
     uint32_t blocks = 0;
     bool measured = false;
+    uint32_t frames = 0;       // full frames launched since the last measured one
+    bool order_stale = false;  // costs measured since the order was last computed
+    // full frames: the measured durations copied to the host (asynchronously, after the launch) to
+    // decide whether the heaviest block would form a tail
+    uint32_t *h_cost = nullptr;
+    hipEvent_t copied = nullptr;
+    bool copy_pending = false, decided = false, tail = false;
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -488,6 +505,7 @@ struct Frame {
   int mode = 0;
   bool ab_alias = false, big = false, share = false;
   bool degenerate = false;
+  vr_context::Schedule *sched_copy = nullptr;  // a timed full-frame launch: copy its durations back
 };
 
 
@@ -692,8 +710,11 @@ void free_views(vr_context *h) {
 
 void free_schedules(vr_context *h) {
   for (auto &kv : h->sched) {
+    if (kv.second.copied) (void)hipEventSynchronize(kv.second.copied);
     if (kv.second.d_cost) (void)hipFree(kv.second.d_cost);
     if (kv.second.d_order) (void)hipFree(kv.second.d_order);
+    if (kv.second.h_cost) (void)hipHostFree(kv.second.h_cost);
+    if (kv.second.copied) (void)hipEventDestroy(kv.second.copied);
   }
   h->sched.clear();
 }
@@ -763,14 +784,27 @@ void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
 // launches (< VR_SCHED_ROUNDS K = 1 waves per device wave slot): with many rounds the tail is a
 // small part of the frame and the row-major order keeps neighbouring tiles (which share voxels in
 // L2) running together (metric frame: 43.6 ms row-major, 45.0 ms sorted).
-bool want_schedule(const vr::RenderParams &P) {
+// Full frames (>= VR_SCHED_ROUNDS) follow a heavy-first schedule (order_heavy_kernel: the previous
+// launch's heaviest blocks first, the rest row-major): a block of rays grazing dense structure can
+// last a whole frame (33 ms of 36 at rotate(30,10,0)) and, started in row-major order, forms a tail
+// the rest of the frame cannot fill.  VR_SCHED=0: no schedule; VR_SCHED_FULL=0: none for full frames.
+bool short_launch(const vr::RenderParams &P) {
   const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) / device_wave_slots();
-  return P.views < 2 && (env_flag("VR_SCHED") || (!env_flag_off("VR_SCHED") && rounds < VR_SCHED_ROUNDS));
+  return rounds < VR_SCHED_ROUNDS;
+}
+bool want_schedule(const vr::RenderParams &P) {
+  if (P.views >= 2 || env_flag_off("VR_SCHED")) return false;
+  return env_flag("VR_SCHED") || short_launch(P) || !env_flag_off("VR_SCHED_FULL");
+}
+
+// launch_order's tail argument: (tail_pct << 32) | resident workgroups; tail_pct 0 = heavy-first.
+uint64_t wg_tail_arg(uint32_t tail_pct) {
+  return (uint64_t)tail_pct << 32 | (uint64_t)(device_wave_slots() / 16 * 6);
 }
 
 // Attach the schedule of this launch shape (`extra` tells launches of one shape apart, e.g. the
 // slab and sweep of a sort-last launch) to P: wg_order / wg_cost / sched_blocks / prio_blocks.
-hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, const Frame &F, int K, hipStream_t stream,
+hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, hipStream_t stream,
                            const char *extra) {
   typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
   static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
@@ -793,19 +827,80 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, const Frame &F, i
     S.blocks = nb;
   }
   if (!(S.d_cost && S.blocks == nb)) return hipSuccess;
-  hipError_t rc;
-  if (S.measured) {
-    rc = vr::launch_order(S.d_cost, nb, S.d_order, stream);
-  } else {  // first launch of this shape: row-major order, durations recorded
-    rc = vr::launch_iota(S.d_order, nb, stream);
-    S.measured = true;
+  hipError_t rc = hipSuccess;
+  const bool full = !short_launch(P) && !env_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
+  if (!full) {  // short launch: every launch measured, ordered longest first by the previous one
+    P.sched_full = 0;
+    if (S.measured) {
+      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, 0u, 0u);
+    } else {  // first launch of this shape: row-major order, durations recorded
+      rc = vr::launch_iota(S.d_order, nb, stream);
+      S.measured = true;
+    }
+  } else {
+    // full frame: the block durations are measured on the first launch of the shape and every
+    // VR_SCHED_REMEASURE-th after (a scheduled full-frame kernel costs ~5 %, so it runs only when
+    // needed) and copied to the host after the launch; once they arrive, the host decides whether
+    // the heaviest block would form a tail (>= VR_SCHED_TAIL_PCT % of the packed frame: the sum of
+    // durations over the resident workgroups).  Tail: the frames follow the heavy-first order
+    // (order_heavy_kernel) without timing hooks; no tail: no schedule at all (row-major).
+    uint32_t every = VR_SCHED_REMEASURE;
+    if (const char *ev = std::getenv("VR_SCHED_REMEASURE")) every = (uint32_t)std::max(1, std::atoi(ev));
+    uint32_t heavy_div = VR_SCHED_HEAVY_DIV;
+    if (const char *ev = std::getenv("VR_SCHED_HEAVY_DIV")) heavy_div = (uint32_t)std::max(1, std::atoi(ev));
+    uint32_t tail_pct = VR_SCHED_TAIL_PCT;
+    if (const char *ev = std::getenv("VR_SCHED_TAIL_PCT")) tail_pct = (uint32_t)std::max(0, std::atoi(ev));
+    if (!S.h_cost) {
+      if (hipHostMalloc(reinterpret_cast<void **>(&S.h_cost), nb * sizeof(uint32_t)) != hipSuccess ||
+          hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return hipSuccess;  // no schedule
+      }
+    }
+    if (S.copy_pending && hipEventQuery(S.copied) == hipSuccess) {  // the last measurement arrived
+      S.copy_pending = false;
+      uint64_t sum = 0;
+      uint32_t mx = 0;
+      for (uint32_t i = 0; i < nb; ++i) {
+        sum += S.h_cost[i];
+        mx = std::max(mx, S.h_cost[i]);
+      }
+      const uint64_t wg_slots = std::max<uint64_t>(1, (uint64_t)(device_wave_slots() / 16 * 6));
+      S.tail = (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
+      S.decided = true;
+      S.order_stale = true;
+    }
+    (void)hipGetLastError();
+    bool measure = !S.measured;
+    if (S.measured && !S.copy_pending && ++S.frames >= every) measure = true;
+    if (measure) {
+      S.frames = 0;
+      if (S.decided && S.tail) {  // measured in the heavy-first order the frames use
+        if (S.order_stale) rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
+      } else {
+        rc = vr::launch_iota(S.d_order, nb, stream);
+      }
+      S.order_stale = false;
+      S.measured = true;
+      P.sched_full = 1;  // timed; the durations are copied back after the launch
+      F.sched_copy = &S;
+    } else if (S.decided && S.tail) {
+      if (S.order_stale) {
+        rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
+        S.order_stale = false;
+      }
+      P.sched_full = 2;  // the heavy-first order, untimed
+    } else {
+      return hipSuccess;  // no tail (or not known yet): the unscheduled row-major launch
+    }
   }
   if (rc != hipSuccess) return rc;
   P.wg_order = S.d_order;
   P.wg_cost = S.d_cost;
   P.sched_blocks = nb;
-  // the first round of workgroups (the longest ones) at raised wave priority (A/B: VR_PRIO_BLOCKS)
-  P.prio_blocks = (uint32_t)(device_wave_slots() / 4);
+  // the first round of workgroups (the longest ones) at raised wave priority (A/B: VR_PRIO_BLOCKS);
+  // none for a full frame, whose first blocks are only the heavy ones
+  P.prio_blocks = P.sched_full ? 0u : (uint32_t)(device_wave_slots() / 4);
   if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
   return hipSuccess;
 }
@@ -914,6 +1009,13 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       P.view_blocks = vfns[ki](P);
     }
     VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
+    if (F.sched_copy) {  // a timed full frame: its block durations to the host, for the tail test
+      vr_context::Schedule &S = *F.sched_copy;
+      VR_HIP(hipMemcpyAsync(S.h_cost, S.d_cost, (size_t)S.blocks * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+      VR_HIP(hipEventRecord(S.copied, stream));
+      S.copy_pending = true;
+      F.sched_copy = nullptr;
+    }
     if (P.wg_cost) {
       if (const char *dump = std::getenv("VR_SCHED_DUMP")) {  // diagnostics: append block durations
         std::vector<uint32_t> c(P.sched_blocks);
@@ -1010,7 +1112,7 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   L.device = h->device;
   bind_reads(L);
   stage_frame(L, P, g_tex.lights);
-  if (K > 1 && want_schedule(P)) {  // a tile of a sweep is a short launch: longest-first schedule
+  if (K > 1 && want_schedule(P) && short_launch(P)) {  // a tile of a sweep: longest-first schedule
     char extra[120];
     std::snprintf(extra, sizeof extra, "slab/%llu/%llu/%g/%g/%d", (unsigned long long)sl->depth,
                   (unsigned long long)sl->z_first, sl->z0, sl->z1, sl->direction);

@@ -75,6 +75,9 @@ struct RenderParams {
   const uint32_t *wg_order;
   uint32_t *wg_cost;
   uint32_t sched_blocks;          // length of wg_order / wg_cost (must equal the launch's grid)
+  uint32_t sched_full;            // 0: a short launch's schedule (longest first, timed); full frames
+                                  // (occupancy-capped kernel, heavy blocks first or row-major): 1 timed,
+                                  // 2 following the last measured order without timing
   uint32_t prio_blocks;           // scheduled launch: the first prio_blocks workgroups (the longest)
                                   // run at raised wave priority
   unsigned long long *steps;      // optional sample counter

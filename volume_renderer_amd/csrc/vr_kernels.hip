@@ -455,9 +455,84 @@ __global__ __launch_bounds__(1024) void order_kernel(const uint32_t *__restrict_
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
 }
 
-hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s) {
+// Full-frame schedule: the heavy blocks (measured duration >= max / div) first, longest first, then
+// every other block in ascending (row-major) order -- the bulk keeps the L2 locality of
+// neighbouring tiles running together, and no heavy block starts late enough to form the tail.
+// tail_pct / wg_slots: only when the longest block lasts at least tail_pct % of the packed frame
+// (sum of durations / resident workgroups) does it risk forming a tail; otherwise the order is
+// plain row-major.
+__global__ __launch_bounds__(1024) void order_heavy_kernel(const uint32_t *__restrict__ cost, uint32_t n,
+                                                           uint32_t div, uint32_t tail_pct, uint32_t wg_slots,
+                                                           uint32_t *__restrict__ order) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t scan[1024];
+  __shared__ uint32_t smax, nheavy, base;
+  __shared__ unsigned long long ssum;
+  if (threadIdx.x == 0) {
+    smax = 0;
+    nheavy = 0;
+    ssum = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  uint32_t m = 0;
+  unsigned long long sum = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    m = max(m, cost[i]);
+    sum += cost[i];
+  }
+  atomicMax(&smax, m);
+  atomicAdd(&ssum, sum);
+  __syncthreads();
+  const unsigned long long packed = ssum / (unsigned long long)max(wg_slots, 1u);
+  const bool tail = (unsigned long long)smax * 100ull >= packed * (unsigned long long)tail_pct;
+  // no tail: every block "light", i.e. row-major
+  const uint32_t thr = tail ? max(smax / max(div, 1u), 1u) : 0xffffffffu;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (cost[i] >= thr) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive offsets of the heavy blocks, largest bucket first
+    uint32_t acc = 0;
+    for (int b = 255; b >= 0; --b) {
+      const uint32_t c = hist[b];
+      hist[b] = acc;
+      acc += c;
+    }
+    nheavy = acc;
+    base = acc;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (cost[i] >= thr) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
+  // the rest in ascending block order: a block-wide exclusive scan per chunk of 1024 blocks
+  for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint32_t f = (i < n && cost[i] < thr) ? 1u : 0u;
+    scan[threadIdx.x] = f;
+    __syncthreads();
+    for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
+      const uint32_t v = threadIdx.x >= off ? scan[threadIdx.x - off] : 0u;
+      __syncthreads();
+      scan[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (f) order[base + scan[threadIdx.x] - 1u] = i;
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) base += scan[threadIdx.x];
+    __syncthreads();
+  }
+  (void)nheavy;
+}
+
+// heavy_div 0: longest first (short launches); else the full-frame order of order_heavy_kernel
+// with tail = (tail_pct << 32) | resident workgroups.
+hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s, uint32_t heavy_div,
+                        uint64_t tail) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
+  if (heavy_div)
+    hipLaunchKernelGGL(order_heavy_kernel, dim3(1), dim3(1024), 0, s, cost, n, heavy_div, (uint32_t)(tail >> 32),
+                       (uint32_t)tail, order);
+  else hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
   return hipGetLastError();
 }
 

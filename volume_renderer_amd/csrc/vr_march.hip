@@ -481,7 +481,7 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 #ifndef VR_MARCH_MIN_EU
 #define VR_MARCH_MIN_EU 6
 #endif
-constexpr int march_min_eu(int cap, bool sched) { return (cap <= 1664 && !sched) ? VR_MARCH_MIN_EU : 1; }
+constexpr int march_min_eu(int cap, int sched) { return (cap <= 1664 && sched != 1) ? VR_MARCH_MIN_EU : 1; }
 #ifndef VR_WG_WAVES
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif
@@ -501,15 +501,19 @@ struct TileShape {
   static constexpr int TW = 1 << LW, TH = 1 << (LR - LW);  // tile width, height
 };
 
-// SCHED: the launch follows P.wg_order and records each block's duration in P.wg_cost (a
-// separate instantiation: the hooks cost ~4 % when compiled in, even unused).
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, bool SCHED>
+// SCHED: the launch follows P.wg_order and records each block's duration in P.wg_cost (separate
+// instantiations: the hooks cost when compiled in, even unused).  SCHED 1: a short launch (few
+// rounds; uncapped registers, its longest waves share a SIMD with few others); 2: a full frame
+// (the occupancy cap of the unscheduled kernel); 3: a full frame following the order without
+// recording durations.
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
-  const uint64_t clk0 = SCHED ? __builtin_amdgcn_s_memrealtime() : 0;
+  constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
+  const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : blockIdx.x;  // cost-ordered schedule
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
   if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
@@ -557,7 +561,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     out[kk + plane] = R.sg;
     out[kk + 2 * plane] = R.sb;
   }
-  if (SCHED) {  // this block's duration, for the next launch's schedule
+  if (TIMED) {  // this block's duration, for the next launch's schedule
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
@@ -816,15 +820,22 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   constexpr int K = VR_MARCH_K;
   const dim3 blk(64 * VR_WG_WAVES);
   const bool sched = P.wg_order && P.wg_cost;
+  constexpr int S1 = K > 1 ? 1 : 0, S2 = K > 1 ? 2 : 0, S3 = K > 1 ? 3 : 0;  // scheduled kernels: K > 1
   if (K == 1 && P.steps) {
-    if (big) hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, true, CAP, false>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, false, CAP, false>), grid, blk, 0, s, P);
-  } else if (K > 1 && sched) {  // scheduled launches use depth lanes (few waves per slot)
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, (K > 1)>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, (K > 1)>), grid, blk, 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, true, CAP, 0>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, false, CAP, 0>), grid, blk, 0, s, P);
+  } else if (K > 1 && sched && P.sched_full == 1) {  // a full frame, durations measured
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S2>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S2>), grid, blk, 0, s, P);
+  } else if (K > 1 && sched && P.sched_full == 2) {  // a full frame in the last measured order
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S3>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S3>), grid, blk, 0, s, P);
+  } else if (K > 1 && sched) {  // a short launch (few waves per slot), longest first
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S1>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S1>), grid, blk, 0, s, P);
   } else {
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, false>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, false>), grid, blk, 0, s, P);
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, 0>), grid, blk, 0, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, 0>), grid, blk, 0, s, P);
   }
   return hipGetLastError();
 }
