@@ -29,12 +29,19 @@ struct Ax {
   int i;
   float w;
 };
+// The 8-bit filter weight rint(frac(xb) * 256) / 256 of a coordinate xb with floor fl, as
+// rint(256 xb) / 256 - fl in one fma: 256 xb is exact, 256 fl an even integer (so the rounding,
+// ties to even included, commutes with it), and the result a multiple of 1/256 in [0, 1] --
+// bit-identical, NaN / inf alike, one VALU less than the sub, mul, rint, mul sequence.
+__device__ __forceinline__ float weight8(float xb, float fl) {
+  return fmaf(rintf(xb * 256.f), 1.f / 256.f, -fl);
+}
 template <bool NANCHK = true>
 __device__ __forceinline__ Ax axis(float c, int n, float fn) {
   if (NANCHK) c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
   const float xb = c * fn - 0.5f;
   const float fl = floorf(xb);
-  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
+  const float w = weight8(xb, fl);
   (void)n;
   return Ax{(int)__builtin_amdgcn_fmed3f(fl, -1.f, fn - 1.f), w};
 }
@@ -47,7 +54,7 @@ __device__ __forceinline__ Ax axis_raw(float c, float fn) {
   if (NANCHK) c = (c != c) ? 0.f : c;  // NaN coordinate -> 0
   const float xb = c * fn - 0.5f;
   const float fl = floorf(xb);
-  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
+  const float w = weight8(xb, fl);
   return Ax{(int)fl, w};
 }
 __device__ __forceinline__ Ax clamp_ax(const Ax &a, int n) { return Ax{min(max(a.i, -1), n - 1), a.w}; }
@@ -160,8 +167,7 @@ __device__ __forceinline__ AxF axis_lut(float c, float fn) {
   c = __builtin_amdgcn_fmed3f(c, 0.f, 1.f);
   const float xb = FMA ? fmaf(c, fn, -0.5f) : c * fn - 0.5f;  // FMA: the fast variant's shading
   const float fl = floorf(xb);
-  const float w = rintf((xb - fl) * 256.f) * (1.f / 256.f);
-  return AxF{fl, w};
+  return AxF{fl, weight8(xb, fl)};
 }
 
 // Trilinear fetch from a texture of fewer than 2^22 padded voxels (the illumination LUT): the
