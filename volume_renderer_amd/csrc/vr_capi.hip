@@ -745,6 +745,10 @@ int device_wave_slots() {
 // restages.  Measured on MI355X (ms): tau 2.0 (C2, 1024x768, 3 rounds) K = 4 19.5, K = 2 29.8,
 // K = 8 25.1; tau 1.07 (metric, 7.9 rounds) K = 2 36.5, K = 4 37.6, K = 1 51.7; tau 1.0 (C5,
 // 4096^2, 64 rounds) K = 2 293.6, K = 4 338.5, K = 1 348.7.  K = 1 only for sparse sampling.
+#ifndef VR_XCD_RUN
+#define VR_XCD_RUN 0  // march workgroups -> XCD runs (vr_march.hip xcd_block); 0: dispatch order
+#endif
+
 int depth_lanes(const vr::RenderParams &P) {
   if (const char *ev = std::getenv("VR_DEPTH_LANES")) {
     const int k = std::atoi(ev);
@@ -939,6 +943,8 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   // the oracle's correctly rounded op sequence (bit-identical to oracle/vr_oracle.c up to acosf)
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
   if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
+  P.xcd_run = VR_XCD_RUN;
+  if (const char *ev = std::getenv("VR_XCD_RUN")) P.xcd_run = std::max(0, std::atoi(ev));  // A/B switch
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
   if (d_out2) {
     P.views = 2;

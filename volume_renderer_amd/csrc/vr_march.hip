@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
+#include <algorithm>
 
 #ifndef VR_MARCH_K
 #define VR_MARCH_K 1  // depth lanes of this object file (see below)
@@ -501,6 +503,18 @@ struct TileShape {
   static constexpr int TW = 1 << LW, TH = 1 << (LR - LW);  // tile width, height
 };
 
+// XCD runs: the dispatcher deals workgroup b to XCD b % 8, so row-major blocks b and b + 1 land on
+// different XCDs (and L2s).  With run R > 1, full groups of 8R workgroups are renumbered so that
+// XCD x takes R consecutive blocks of the group (g * 8R + x * R + j, j-th of its turns); the tail
+// keeps dispatch order.  A bijection of the grid: the image is the same for any R.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n, int run) {
+  if (run <= 1) return b;
+  const uint32_t R = (uint32_t)run, gs = 8u * R, g = b / gs;
+  if ((g + 1) * gs > n) return b;
+  const uint32_t r = b - g * gs;
+  return g * gs + (r & 7u) * R + (r >> 3);
+}
+
 // SCHED: the launch follows P.wg_order and records each block's duration in P.wg_cost (separate
 // instantiations: the hooks cost when compiled in, even unused).  SCHED 1: a short launch (few
 // rounds; uncapped registers, its longest waves share a SIMD with few others); 2: a full frame
@@ -514,7 +528,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   float *L = lds[wave];
   constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : blockIdx.x;  // cost-ordered schedule
+  const uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
   if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
   // fused stereo: the second view's workgroups follow the first's (same rays, other eye)
@@ -815,6 +829,16 @@ hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mo
 }
 #endif
 
+// Diagnostics (VR_LDS_PAD=bytes): unused dynamic LDS per workgroup of a short scheduled launch,
+// to cap the workgroups a CU holds (the heavy waves' co-residency).
+static unsigned short_launch_lds_pad() {
+  static const unsigned pad = [] {
+    const char *ev = getenv("VR_LDS_PAD");
+    return ev ? (unsigned)std::max(0, atoi(ev)) : 0u;
+  }();
+  return pad;
+}
+
 template <int MODE, bool AB, bool SH, int CAP>
 static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
   constexpr int K = VR_MARCH_K;
@@ -831,8 +855,9 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
     if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S3>), grid, blk, 0, s, P);
     else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S3>), grid, blk, 0, s, P);
   } else if (K > 1 && sched) {  // a short launch (few waves per slot), longest first
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S1>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S1>), grid, blk, 0, s, P);
+    const unsigned pad = short_launch_lds_pad();
+    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S1>), grid, blk, pad, s, P);
+    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S1>), grid, blk, pad, s, P);
   } else {
     if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, 0>), grid, blk, 0, s, P);
     else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, 0>), grid, blk, 0, s, P);
