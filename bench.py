@@ -156,12 +156,16 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
+    timed_kernels = {}  # march kernel instantiation -> timed frames that launched it
+
     def frame(i=None):
         if i is not None:
             ev[i][0].record(stream)
         mex.render_device(h, ra, out_local.data_ptr(), part, 0, sptr)
         if i is not None:
             ev[i][1].record(stream)
+            kn = mex.last_march_kernel()
+            timed_kernels[kn] = timed_kernels.get(kn, 0) + 1
         if world > 1:
             dist.gather(out_local, list(gathered.chunk(world)) if rank == 0 else None, dst=0)
             if rank == 0:
@@ -291,6 +295,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel_ms": round(t_kernel_s * 1e3, 3),
+                         "kernel": max(timed_kernels, key=timed_kernels.get) if timed_kernels else None,
+                         "kernels_timed": timed_kernels,
                          "bytes_per_launch": bytes_launch,
                          "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F,
                          "fetched": {"bytes_per_launch": fetched,
@@ -322,7 +328,8 @@ def main():
         try:
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
-            if world == 1 and tj.get("workload") == result["config"]["workload"]:
+            if (world == 1 and tj.get("workload") == result["config"]["workload"]
+                    and tj.get("kernel") == result["roofline"]["kernel"]):
                 src = os.path.relpath(args.traffic_json, ROOT)
                 result["roofline"]["traffic"] = tj["bytes_per_launch"]
                 result["roofline"]["traffic_source"] = src + " (" + tj.get("method", "") + ")"
@@ -410,8 +417,16 @@ def cpu_baseline(args, host_vol, n, W, H, refl, lut, lights, R, gpu_out):
         "one_core": {"value": round(len(cols1) * H / cpu1_s / 1e6, 6), "unit": "Mrays/s", "cores": 1,
                      "sample": f"every {args.cpu_stride_1core}th column ({len(cols1)} cols x {H} rays, "
                                f"{samples1} samples), {cpu1_s:.1f} s"}}
+    import hashlib
+    c, xi, y = np.unravel_index(int(np.argmax(d)), d.shape)
+    x = int(cols[xi])
     parity = {"max_abs": float(d.max()), "img_max": float(np.abs(o[:, cols, :]).max()),
-              "bit_exact_frac": float((g[:, cols, :].view(np.uint32) == o[:, cols, :].view(np.uint32)).mean())}
+              "bit_exact_frac": float((g[:, cols, :].view(np.uint32) == o[:, cols, :].view(np.uint32)).mean()),
+              "max_abs_at": {"x": x, "y": int(y), "channel": "RGB"[int(c)], "product": float(g[c, x, y]),
+                             "oracle": float(o[c, x, y])},
+              "image_sha256": hashlib.sha256(np.ascontiguousarray(g).tobytes()).hexdigest(),
+              "what": "GPU frame vs the oracle (fp32) on every %dth column; image_sha256 = the whole GPU frame's "
+                      "[3][W][H] fp32 bytes" % args.cpu_stride}
     return base, parity
 
 

@@ -279,6 +279,11 @@ int vr_debug_slot_transition(const int32_t idx_in[3], int32_t sim_em_ab, int32_t
 /* Last error message of this thread ("" if none). */
 const char *vr_last_error(void);
 
+/* The demangled name of the march kernel instantiation the last render launched (the process's
+ * last staged-march launch), e.g. "vr::fast::march_kernel<2, 1, true, false, true, false, 1664, 0>":
+ * bench.py names the kernel it times with it and keys the profiler's counters to it. */
+int vr_last_march_kernel(char *buf, size_t buflen);
+
 /* Library build identification ("libvrhip <version> gfx950 ..."). */
 const char *vr_version(void);
 

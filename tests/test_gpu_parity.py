@@ -374,6 +374,8 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
             monkeypatch.setenv(k, val)
+        if env.get("VR_DEPTH_LANES") == "8" and vr.mex.depth_lanes(64, 64) != 8:
+            continue  # K = 8 is built only in a diagnostic build (make DIAG=1)
         imgs[name] = r.render()
     base = imgs["default"]
     assert base.max() > 0

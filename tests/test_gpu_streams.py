@@ -101,3 +101,33 @@ def test_volume_upload_while_previous_frame_renders(device_data):
         want = serial[k % 2].reshape(-1, order="F")
         assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32)), k
     vr.volumeRender("delete", h)
+
+
+def test_overlapping_readers_keep_the_volume_until_the_last_one():
+    """Two renders of one volume in flight on two streams, the later-issued one much shorter: when
+    it has finished, the earlier (longer) one still reads the buffer, so a re-upload of changed data
+    of the same size must not rewrite it in place (every in-flight reader is tracked, not only the
+    newest launch's event).  The long frame equals its serial render."""
+    n = 256
+    data = [O.shell_volume(n), np.asfortranarray(O.shell_volume(n)[::-1, :, :] * np.float32(0.7))]
+    lut = _stamped(vr.HenyeyGreenstein(32), 5)
+    re = _stamped(np.float32(1.0), 6)
+    big, small = (2048, 2048), (16, 16)
+    h = vr.volumeRender("new")
+    v0 = _stamped(data[0], 100)
+    vr.volumeRender("sync_volumes", h, np.uint64(1), v0, re, v0)
+    want = vr.volumeRender("render", h, *_args(LIGHTS_A, lut, big)).reshape(-1, order="F")
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    H, W = big
+    o_big = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    o_small = torch.empty(3 * small[0] * small[1], dtype=torch.float32, device="cuda")
+    ra, k1 = mex.render_args(*_args(LIGHTS_A, lut, big))
+    rs, k2 = mex.render_args(*_args(LIGHTS_A, lut, small))
+    mex.render_device(h, ra, o_big.data_ptr(), None, 0, sa.cuda_stream)
+    mex.render_device(h, rs, o_small.data_ptr(), None, 0, sb.cuda_stream)
+    sb.synchronize()  # the newest reader is done; the first one is most likely still running
+    v1 = _stamped(data[1], 200)
+    vr.volumeRender("sync_volumes", h, np.uint64(1), v1, re, v1)  # same size: the in-place candidate
+    torch.cuda.synchronize()
+    assert np.array_equal(o_big.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    vr.volumeRender("delete", h)

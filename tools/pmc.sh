@@ -6,7 +6,9 @@
 OUT=$1; shift
 cd /tmp; export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline --pipelined-streams 0 $*"
+# --warmup 1: the first full frame of a shape is the timed-schedule instantiation (SCHED 2); the
+# production frames that bench.py times come after it
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --pipelined-streams 0 $*"
 i=0
 PMCG=${PMC_GROUPS:-"SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_INSTS_LDS,SQ_INSTS_SALU,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_INSTS_SMEM;SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_LDS,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE;FETCH_SIZE;TCC_HIT_sum,TCC_MISS_sum,TCC_REQ_sum;GRBM_GUI_ACTIVE,SQ_INSTS_VALU_TRANS_F32,SQ_THREAD_CYCLES_VALU"}
 IFS=';' read -ra GRPS <<< "$PMCG"

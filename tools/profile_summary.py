@@ -44,25 +44,48 @@ with open(os.path.join(out, "pmc_summary.txt"), "w") as fh:
     fh.write("\n".join(lines) + "\n")
 
 
-def mean(kpattern, counter):
-    xs = [v for k, cs in vals.items() if re.search(kpattern, k) for v in cs.get(counter, {}).values()]
+def mean(kname, counter):
+    """Per-dispatch mean of a counter over the dispatches of exactly the kernel `kname`."""
+    xs = [v for k, cs in vals.items() if k.split("(")[0].replace("void ", "", 1) == kname
+          for v in cs.get(counter, {}).values()]
     return sum(xs) / len(xs) if xs else None
 
 
-# metric config: march_kernel<K, MODE 1, absorption aliases emission, no counters, half-texel launch or not, 32-bit, slot, unscheduled or full-frame schedule>
-march = r"march_kernel<\d, 1, true, false, (?:true|false), false, \d+, (?:false|0|2)>"
-fetch_kb, write_kb = mean(march, "FETCH_SIZE"), mean(march, "WRITE_SIZE")
-if fetch_kb is not None:
+# the kernel bench.py timed (its roofline.kernel, the exact instantiation), else the most-launched
+# march kernel of the kernel trace
+kname = None
+try:
+    with open(os.path.join(run, "bench.json")) as fh:
+        kname = json.loads(fh.read().strip().splitlines()[-1])["roofline"].get("kernel")
+except (OSError, ValueError, KeyError, IndexError):
+    pass
+if kname is None and ks:
+    with open(ks[0]) as fh:
+        rows = [r for r in csv.DictReader(fh) if "march_kernel<" in r["Name"]]
+    if rows:
+        kname = max(rows, key=lambda r: int(r["Calls"]))["Name"].split("(")[0].replace("void ", "", 1)
+fetch_kb, write_kb = (mean(kname, "FETCH_SIZE"), mean(kname, "WRITE_SIZE")) if kname else (None, None)
+if fetch_kb is None:
+    print("no PMC dispatches of", kname)
+else:
     traffic = 2 * 1024 * fetch_kb + 1024 * (write_kb or 0.0)
-    extra = {c: mean(march, c) for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU",
+    extra = {c: mean(kname, c) for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU",
+                                          "SQ_INSTS_SMEM", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                                          "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY",
                                           "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_ACTIVE_INST_VALU",
-                                          "TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum", "GRBM_GUI_ACTIVE")}
+                                          "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS", "SQ_INSTS_VALU_TRANS_F32",
+                                          "SQ_THREAD_CYCLES_VALU", "TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum",
+                                          "GRBM_GUI_ACTIVE")}
+    ndisp = {c: len([1 for k, cs in vals.items() if k.split("(")[0].replace("void ", "", 1) == kname
+                     for _ in cs.get(c, {})]) for c in ("FETCH_SIZE", "SQ_INSTS_VALU")}
     with open(os.path.join(out, "traffic.json"), "w") as fh:
-        json.dump({"workload": workload, "kernel": march, "fetch_size_kib": fetch_kb, "write_size_kib": write_kb,
+        json.dump({"workload": workload, "kernel": kname, "dispatches": ndisp,
+                   "fetch_size_kib": fetch_kb, "write_size_kib": write_kb,
                    "bytes_per_launch": traffic,
                    "valu_insts_per_launch": extra["SQ_INSTS_VALU"],
                    "counters_per_launch": {k: v for k, v in extra.items() if v is not None},
-                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; read bytes = 2 x 1024 x FETCH_SIZE "
-                             "(gfx950 64 B tally per 128 B request)"}, fh, indent=1)
-    print("traffic bytes/launch", traffic)
+                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py's production "
+                             "frames (the timed instantiation, matched by exact name); read bytes = "
+                             "2 x 1024 x FETCH_SIZE (gfx950 64 B tally per 128 B request)"}, fh, indent=1)
+    print("kernel", kname, "traffic bytes/launch", traffic)
 print("\n".join(lines[:80]))

@@ -1,0 +1,15 @@
+#!/bin/bash
+# tools/r3.sh RUN [ablation variants...] -- round-3 measurement pass on the GPU box (via gpurun):
+# GPU tests, the default bench line, rocprofv3 kernel trace, PMC passes on the timed kernel, and
+# (with variants) the full-size shading ablation.  Outputs under gpurun_out/RUN.
+RUN=${1:-r3}; shift
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$RUN &&
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/$RUN/tests.log 2>&1 &&
+timeout -k 10 400 python bench.py > gpurun_out/$RUN/bench.json 2> gpurun_out/$RUN/bench.err &&
+(cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
+ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$RUN/kt -o kt --output-format csv -- \
+   python bench.py --steps 10 --warmup 2 --no-cpu-baseline --pipelined-streams 0 > gpurun_out/$RUN/kt.log 2>&1) &&
+PMC_GROUPS="FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum,TCC_MISS_sum,TCC_REQ_sum;SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_INSTS_LDS,SQ_INSTS_SALU,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_INSTS_SMEM;SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_LDS,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE;GRBM_GUI_ACTIVE,SQ_INSTS_VALU_TRANS_F32,SQ_THREAD_CYCLES_VALU" \
+  bash tools/pmc.sh gpurun_out/$RUN/pmc &&
+if [ $# -gt 0 ]; then timeout -k 10 900 python -u tools/shade_ablation.py gpurun_out/$RUN/ablation.json "$@" > gpurun_out/$RUN/ablation.log 2>&1; fi &&
+tail -3 gpurun_out/$RUN/tests.log && cat gpurun_out/$RUN/bench.json

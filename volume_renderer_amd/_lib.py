@@ -97,6 +97,7 @@ SIGNATURES = [
     ("vr_debug_slot_transition", c_int, [POINTER(c_int32), c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                          POINTER(c_int32), POINTER(c_int32)]),
     ("vr_last_error", c_char_p, []),
+    ("vr_last_march_kernel", c_int, [c_char_p, c_size_t]),
     ("vr_version", c_char_p, []),
 ]
 

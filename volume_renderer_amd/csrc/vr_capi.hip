@@ -31,6 +31,15 @@
 #include "vr_device.h"
 #include "vr_resources.h"
 
+#ifndef VR_WITH_K8
+#define VR_WITH_K8 0  // the K = 8 march objects (diagnostic build, make DIAG=1)
+#endif
+#if VR_WITH_K8
+#define VR_K8(k8, k4) k8
+#else
+#define VR_K8(k8, k4) k4  // never selected: depth_lanes returns 8 only in a K = 8 build
+#endif
+
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
 // vr_march.hip built with VR_MARCH_FAST=1 / 0 (namespaces fast / exact) and VR_MARCH_K = 1, 2, 4, 8
@@ -99,6 +108,20 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 #define VR_SCHED_ROUNDS 6.0      // longest-first schedule below this many K = 1 waves per wave slot
 #endif
 
+namespace vr {
+std::string &last_march_kernel() {
+  static std::string name;
+  return name;
+}
+void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched) {
+  char b[160];
+  auto tf = [](bool v) { return v ? "true" : "false"; };
+  std::snprintf(b, sizeof b, "vr::%s::march_kernel<%d, %d, %s, %s, %s, %s, %d, %d>", fast ? "fast" : "exact", K, mode,
+                tf(ab), tf(count), tf(share), tf(big), cap, sched);
+  last_march_kernel() = b;
+}
+}  // namespace vr
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -160,13 +183,13 @@ struct DevBuf {
   // the MATLAB Volume it was uploaded from (VolRec identity: data pointer, TimeLastUpdate, size)
   const float *src_data = nullptr;
   uint64_t src_last_update = 0, src_bytes = 0;
-  // completion of the last launch that reads it (vr_resources.h): it is neither rewritten nor freed
-  // before then
-  vr_host::EventPtr last_use;
+  // completions of the launches / peer copies that read it (vr_resources.h): it is neither
+  // rewritten nor freed before all of them
+  vr_host::Readers readers;
   // multi-device group (vr_new_multi): its copies on the other devices, and the version each copies
   std::map<int, std::shared_ptr<DevBuf>> replicas;
   std::map<int, uint64_t> replica_of;
-  ~DevBuf() { vr_host::pooled_free(ptr, bytes, device, last_use); }
+  ~DevBuf() { vr_host::pooled_free(ptr, bytes, device, std::move(readers)); }
 };
 using BufPtr = std::shared_ptr<DevBuf>;
 
@@ -287,7 +310,7 @@ void sync_volume(vr_context *h, int tex, int slot) {
   const uint64_t n = v.dims[0] * v.dims[1] * v.dims[2];
   const uint64_t padded = n ? (v.dims[0] + 2) * (v.dims[1] + 2) * (v.dims[2] + 2) * sizeof(float) : 0;
   BufPtr b = h->buf[slot];
-  if (!(b && b.use_count() == 2 && b->bytes == padded && b->device == h->device && vr_host::done(b->last_use))) {
+  if (!(b && b.use_count() == 2 && b->bytes == padded && b->device == h->device && b->readers.done())) {
     h->buf[slot].reset();
     b = std::make_shared<DevBuf>();
     b->device = h->device;
@@ -297,7 +320,7 @@ void sync_volume(vr_context *h, int tex, int slot) {
   for (int i = 0; i < 3; ++i) b->dims[i] = v.dims[i];
   b->nonfinite = false;
   b->maxabs = 0.f;
-  b->last_use.reset();
+  b->readers.clear();  // a fresh buffer, or one whose readers all completed
   if (n) {
     if (!v.data) throw HipError{hipErrorInvalidValue, "volume data is NULL"};
     vr_host::Uploader &U = vr_host::uploaders()[h->device];
@@ -752,7 +775,7 @@ int device_wave_slots() {
 int depth_lanes(const vr::RenderParams &P) {
   if (const char *ev = std::getenv("VR_DEPTH_LANES")) {
     const int k = std::atoi(ev);
-    if (k == 1 || k == 2 || k == 4 || k == 8) return k;
+    if (k == 1 || k == 2 || k == 4 || (k == 8 && VR_WITH_K8)) return k;
   }
   const double waves = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0);  // at K = 1
   const double rounds = waves / device_wave_slots();
@@ -812,7 +835,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
                            const char *extra) {
   typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
   static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
-                                    vr::fast::march_blocks_k8};
+                                    VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
   const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
   const uint32_t nb = bfns[ki](P);
   // keyed by stream too: the order buffer of one stream is never rewritten under another's launch
@@ -1005,13 +1028,17 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     typedef hipError_t (*launch_fn)(const vr::RenderParams &, int, bool, bool, bool, hipStream_t);
     typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
     static const launch_fn fns[2][4] = {
-        {vr::exact::launch_march_k1, vr::exact::launch_march_k2, vr::exact::launch_march_k4, vr::exact::launch_march_k8},
-        {vr::fast::launch_march_k1, vr::fast::launch_march_k2, vr::fast::launch_march_k4, vr::fast::launch_march_k8}};
+        {vr::exact::launch_march_k1, vr::exact::launch_march_k2, vr::exact::launch_march_k4,
+         VR_K8(vr::exact::launch_march_k8, vr::exact::launch_march_k4)},
+        {vr::fast::launch_march_k1, vr::fast::launch_march_k2, vr::fast::launch_march_k4,
+         VR_K8(vr::fast::launch_march_k8, vr::fast::launch_march_k4)}};
     const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
-    if (!P.steps && K > 1 && want_schedule(P)) VR_HIP(attach_schedule(h, P, F, K, stream, ""));
+    // (the exact-arithmetic variant is a parity reference: built without the scheduled kernels)
+    if (!P.steps && K > 1 && P.fast_shade && want_schedule(P)) VR_HIP(attach_schedule(h, P, F, K, stream, ""));
     if (P.views > 1) {
       static const blocks_fn vfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
-                                        vr::fast::march_blocks_k4, vr::fast::march_blocks_k8};
+                                        vr::fast::march_blocks_k4,
+                                        VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
       P.view_blocks = vfns[ki](P);
     }
     VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
@@ -1138,7 +1165,7 @@ BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
   if (b->device == dev && !env_flag("VR_GROUP_REPLICATE")) return b;  // test switch: copy on one device too
   BufPtr &r = b->replicas[dev];
   if (r && r->bytes == b->bytes && b->replica_of[dev] == b->version) return r;
-  if (!(r && r->bytes == b->bytes && vr_host::done(r->last_use))) {
+  if (!(r && r->bytes == b->bytes && r->readers.done())) {
     r = std::make_shared<DevBuf>();
     r->device = dev;
     r->bytes = b->bytes;
@@ -1147,7 +1174,14 @@ BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
       VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&r->ptr), b->bytes, dev));
     }
   }
-  if (b->bytes) VR_HIP(hipMemcpyPeerAsync(r->ptr, dev, b->ptr, b->device, b->bytes, s));
+  if (b->bytes) {
+    VR_HIP(hipMemcpyPeerAsync(r->ptr, dev, b->ptr, b->device, b->bytes, s));
+    // the copy reads b and writes r: neither is rewritten, pooled or freed before it completes
+    vr_host::EventPtr ev;
+    VR_HIP(vr_host::record_event(s, ev));
+    b->readers.add(ev);
+    r->readers.add(ev);
+  }
   for (int i = 0; i < 3; ++i) r->dims[i] = b->dims[i];
   r->nonfinite = b->nonfinite;
   r->maxabs = b->maxabs;
@@ -1203,7 +1237,9 @@ int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream
     VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&h->d_part), (size_t)n * part_floats * sizeof(float)));
     h->d_part_bytes = (size_t)n * part_floats * sizeof(float);
   }
-  // the primary's part first: it uploads the frame's lights / LUT and binds them
+  // the primary's part first: it uploads the frame's lights / LUT and binds them.  Slot 0 of the
+  // part buffer is read by the previous frame's assembly, which may run on another stream.
+  VR_HIP(hipStreamWaitEvent(stream, h->gdone, 0));
   Frame F0;
   int rc = do_render(h, a, &p0, h->d_part, nullptr, stream, F0);
   if (rc) return rc;
@@ -1935,19 +1971,35 @@ int vr_resize_device(const float *d_in, const uint64_t in_dims[3], const uint64_
   }
   uint64_t cur[3] = {in_dims[0], in_dims[1], in_dims[2]};
   const float *src = d_in;
-  std::vector<void *> temps;
+  // the device temporaries and the host contributions their copies read: all kept until the stream
+  // has drained (the final synchronize, or the guard's on an error part-way)
+  struct Temps {
+    hipStream_t s;
+    std::vector<void *> dev;
+    std::vector<std::vector<double>> w;
+    std::vector<std::vector<int32_t>> idx;
+    ~Temps() {  // stream-ordered frees after the passes, then the host data is released
+      for (void *t : dev) (void)hipFreeAsync(t, s);
+      (void)hipStreamSynchronize(s);
+      (void)hipGetLastError();
+    }
+  } temps{s, {}, {}, {}};
+  temps.w.reserve(passes.size());
+  temps.idx.reserve(passes.size());
   for (size_t k = 0; k < passes.size(); ++k) {
     const int dim = passes[k];
-    std::vector<double> w;
-    std::vector<int32_t> idx;
+    temps.w.emplace_back();
+    temps.idx.emplace_back();
+    std::vector<double> &w = temps.w.back();
+    std::vector<int32_t> &idx = temps.idx.back();
     int32_t P = 0;
     resize_contributions(cur[dim], out_dims[dim], w, idx, P);
     double *d_w = nullptr;
     int32_t *d_idx = nullptr;
     VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_w), w.size() * sizeof(double), s));
+    temps.dev.push_back(d_w);
     VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_idx), idx.size() * sizeof(int32_t), s));
-    temps.push_back(d_w);
-    temps.push_back(d_idx);
+    temps.dev.push_back(d_idx);
     VR_HIP(hipMemcpyAsync(d_w, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice, s));
     VR_HIP(hipMemcpyAsync(d_idx, idx.data(), idx.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
     uint64_t nxt[3] = {cur[0], cur[1], cur[2]};
@@ -1955,15 +2007,13 @@ int vr_resize_device(const float *d_in, const uint64_t in_dims[3], const uint64_
     float *dst = d_out;
     if (k + 1 < passes.size()) {
       VR_HIP(hipMallocAsync(reinterpret_cast<void **>(&dst), nxt[0] * nxt[1] * nxt[2] * sizeof(float), s));
-      temps.push_back(dst);
+      temps.dev.push_back(dst);
     }
     VR_HIP(vr::launch_resize_dim(src, cur, dim, out_dims[dim], d_w, d_idx, P, dst, s));
     src = dst;
     for (int i = 0; i < 3; ++i) cur[i] = nxt[i];
   }
-  for (void *t : temps) VR_HIP(hipFreeAsync(t, s));
-  VR_HIP(hipStreamSynchronize(s));  // the host contributions are borrowed by the copies
-  return VR_OK;
+  return VR_OK;  // ~Temps: free, then synchronize
   VR_GUARD_END
 }
 
@@ -2017,6 +2067,17 @@ uint64_t vr_timestamp(void) {
 }
 
 const char *vr_last_error(void) { return g_last_error.c_str(); }
+
+int vr_last_march_kernel(char *buf, size_t buflen) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const std::string &s = vr::last_march_kernel();
+  if (buf && buflen) {
+    const size_t n = std::min(buflen - 1, s.size());
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return VR_OK;
+}
 
 const char *vr_version(void) { return "libvrhip 0.1 gfx950 (MI355X) volume ray-marcher"; }
 

@@ -104,4 +104,9 @@ struct BufStats {
   float maxabs;
 };
 
+// Host side: the demangled name of the march kernel a launch entry just enqueued (vr_capi.hip;
+// read back by vr_last_march_kernel, so that bench.py can name the kernel it times and match the
+// profiler's counters to exactly that instantiation).
+void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched);
+
 }  // namespace vr

@@ -844,24 +844,34 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   constexpr int K = VR_MARCH_K;
   const dim3 blk(64 * VR_WG_WAVES);
   const bool sched = P.wg_order && P.wg_cost;
-  constexpr int S1 = K > 1 ? 1 : 0, S2 = K > 1 ? 2 : 0, S3 = K > 1 ? 3 : 0;  // scheduled kernels: K > 1
+  // scheduled kernels: K > 1, fast variant only (otherwise the names below alias the SCHED 0 kernel)
+  constexpr bool SCH = K > 1 && VR_MARCH_FAST;
+  constexpr int S1 = SCH ? 1 : 0, S2 = SCH ? 2 : 0, S3 = SCH ? 3 : 0;
+#define VR_LAUNCH(KK, CNT, BG, SC, PAD)                                                                    \
+  do {                                                                                                    \
+    hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, PAD, s, P);        \
+    note_march_kernel(VR_MARCH_FAST, KK, MODE, AB, CNT, SH, BG, CAP, SC);                                 \
+  } while (0)
   if (K == 1 && P.steps) {
-    if (big) hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, true, CAP, 0>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<1, MODE, AB, true, SH, false, CAP, 0>), grid, blk, 0, s, P);
+    if (big) VR_LAUNCH(1, true, true, 0, 0);
+    else VR_LAUNCH(1, true, false, 0, 0);
+  } else if (!VR_MARCH_FAST && sched) {  // the exact variant is built without the scheduled kernels
+    return hipErrorInvalidValue;
   } else if (K > 1 && sched && P.sched_full == 1) {  // a full frame, durations measured
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S2>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S2>), grid, blk, 0, s, P);
+    if (big) VR_LAUNCH(K, false, true, S2, 0);
+    else VR_LAUNCH(K, false, false, S2, 0);
   } else if (K > 1 && sched && P.sched_full == 2) {  // a full frame in the last measured order
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S3>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S3>), grid, blk, 0, s, P);
+    if (big) VR_LAUNCH(K, false, true, S3, 0);
+    else VR_LAUNCH(K, false, false, S3, 0);
   } else if (K > 1 && sched) {  // a short launch (few waves per slot), longest first
     const unsigned pad = short_launch_lds_pad();
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, S1>), grid, blk, pad, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, S1>), grid, blk, pad, s, P);
+    if (big) VR_LAUNCH(K, false, true, S1, pad);
+    else VR_LAUNCH(K, false, false, S1, pad);
   } else {
-    if (big) hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, true, CAP, 0>), grid, blk, 0, s, P);
-    else hipLaunchKernelGGL((march_kernel<K, MODE, AB, false, SH, false, CAP, 0>), grid, blk, 0, s, P);
+    if (big) VR_LAUNCH(K, false, true, 0, 0);
+    else VR_LAUNCH(K, false, false, 0, 0);
   }
+#undef VR_LAUNCH
   return hipGetLastError();
 }
 

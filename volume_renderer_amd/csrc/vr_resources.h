@@ -62,10 +62,42 @@ inline void wait(const EventPtr &ev) {
   if (ev && ev->e) (void)hipEventSynchronize(ev->e);
 }
 
+// Every pending reader of one buffer (the completion events of the launches and peer copies that
+// read it, on any streams).  A buffer is rewritten, pooled for reuse or freed only when all of them
+// have completed: launches on different streams finish in any order, so the newest event alone
+// says nothing about the older ones.
+struct Readers {
+  std::vector<EventPtr> evs;
+  void prune() {
+    size_t k = 0;
+    for (size_t i = 0; i < evs.size(); ++i)
+      if (!vr_host::done(evs[i])) evs[k++] = evs[i];
+    evs.resize(k);
+  }
+  void add(const EventPtr &ev) {
+    prune();
+    if (ev && ev->e) evs.push_back(ev);
+  }
+  bool done() {
+    prune();
+    return evs.empty();
+  }
+  void wait() {
+    for (const EventPtr &ev : evs) vr_host::wait(ev);
+    evs.clear();
+  }
+  void clear() { evs.clear(); }
+};
+inline Readers readers_of(const EventPtr &ev) {
+  Readers r;
+  r.add(ev);
+  return r;
+}
+
 struct Retired {
   void *ptr;
   int device;
-  EventPtr ev;
+  Readers ev;
   bool pinned;
 };
 
@@ -85,13 +117,13 @@ inline void release(void *ptr, int device, bool pinned) {
   if (cur != device) (void)hipSetDevice(cur);
 }
 
-// free now if no launch still reads the allocation, else when `ev` completes
-inline void free_when_done(void *ptr, int device, const EventPtr &ev, bool pinned = false) {
+// free now if no launch still reads the allocation, else when all its readers complete
+inline void free_when_done(void *ptr, int device, Readers ev, bool pinned = false) {
   if (!ptr) return;
-  if (done(ev))
+  if (ev.done())
     release(ptr, device, pinned);
   else
-    retired().push_back({ptr, device, ev, pinned});
+    retired().push_back({ptr, device, std::move(ev), pinned});
 }
 
 // release what has completed; block = wait for everything first (before a retried allocation)
@@ -99,8 +131,8 @@ inline void prune_retired(bool block = false) {
   auto &r = retired();
   size_t k = 0;
   for (size_t i = 0; i < r.size(); ++i) {
-    if (block) wait(r[i].ev);
-    if (done(r[i].ev))
+    if (block) r[i].ev.wait();
+    if (r[i].ev.done())
       release(r[i].ptr, r[i].device, r[i].pinned);
     else
       r[k++] = r[i];
@@ -116,7 +148,7 @@ struct Pooled {
   void *ptr;
   int device;
   size_t bytes;
-  EventPtr ev;
+  Readers ev;
 };
 constexpr size_t POOL_MIN = 1ull << 20, POOL_MAX = 64ull << 30;
 
@@ -138,7 +170,7 @@ inline void pool_clear(int device = -1) {
   size_t k = 0;
   for (size_t i = 0; i < p.size(); ++i) {
     if (device < 0 || p[i].device == device) {
-      wait(p[i].ev);
+      p[i].ev.wait();
       release(p[i].ptr, p[i].device, false);
     } else {
       p[k++] = p[i];
@@ -166,7 +198,7 @@ inline hipError_t device_alloc(void **p, size_t bytes) {
 inline hipError_t pooled_alloc(void **p, size_t bytes, int device) {
   auto &q = pool();
   for (size_t i = 0; i < q.size(); ++i) {
-    if (q[i].device == device && q[i].bytes == bytes && done(q[i].ev)) {
+    if (q[i].device == device && q[i].bytes == bytes && q[i].ev.done()) {
       *p = q[i].ptr;
       q.erase(q.begin() + (ptrdiff_t)i);
       return hipSuccess;
@@ -176,17 +208,17 @@ inline hipError_t pooled_alloc(void **p, size_t bytes, int device) {
 }
 
 // give a volume buffer back: pooled (it stays allocated) unless small or the pool is full
-inline void pooled_free(void *ptr, size_t bytes, int device, const EventPtr &ev) {
+inline void pooled_free(void *ptr, size_t bytes, int device, Readers ev) {
   if (!ptr) return;
   if (bytes < POOL_MIN || bytes > POOL_MAX) {
-    free_when_done(ptr, device, ev);
+    free_when_done(ptr, device, std::move(ev));
     return;
   }
   auto &q = pool();
-  q.push_back({ptr, device, bytes, ev});
+  q.push_back({ptr, device, bytes, std::move(ev)});
   size_t total = pool_bytes(device);
   for (size_t i = 0; i < q.size() && total > POOL_MAX;) {  // oldest completed first
-    if (q[i].device == device && done(q[i].ev) && q[i].ptr != ptr) {
+    if (q[i].device == device && q[i].ptr != ptr && q[i].ev.done()) {
       total -= q[i].bytes;
       release(q[i].ptr, device, false);
       q.erase(q.begin() + (ptrdiff_t)i);
@@ -208,10 +240,15 @@ struct ConstRing {
   unsigned next = 0;
 
   hipError_t init(int d) {
-    if (host) return hipSuccess;
+    if (host && dev) return hipSuccess;
     device = d;
     hipError_t rc = hipHostMalloc(reinterpret_cast<void **>(&host), SLOT * N, hipHostMallocDefault);
     if (rc == hipSuccess) rc = device_alloc(reinterpret_cast<void **>(&dev), SLOT * N);
+    if (rc != hipSuccess) {  // all or nothing: a later call retries (or keeps returning the error)
+      if (host) (void)hipHostFree(host);
+      host = nullptr;
+      dev = nullptr;
+    }
     return rc;
   }
 };
@@ -263,9 +300,9 @@ struct LaunchRec {
       rc = hipStreamSynchronize(stream);
     }
     for (auto &b : reads)
-      if (b) b->last_use = ev;
+      if (b) b->readers.add(ev);
     if (slot >= 0) rings()[device].ev[slot] = ev;
-    if (big) free_when_done(big, device, ev);
+    if (big) free_when_done(big, device, readers_of(ev));
     big = nullptr;
     return rc;
   }

@@ -393,6 +393,9 @@ __device__ __forceinline__ float divpi(float x) {
 #ifndef VR_FAST_NLEN
 #define VR_FAST_NLEN 1  // 1: the fast variant takes the unit normal's length as 1 (shade_lights)
 #endif
+#ifndef VR_FAST_COS
+#define VR_FAST_COS 1  // 1: the fast variant's cosines as dot * rsq * rsq; 0: correctly rounded (ablation)
+#endif
 extern "C" __device__ float __ocml_acospi_f32(float);
 __device__ __forceinline__ float acospi_q(float q) {
 #if VR_FAST_ACOS
@@ -434,6 +437,44 @@ __device__ __forceinline__ float opacity(float a, float tstep) {
 template <bool FAST>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib) {
+#if !VR_FAST_COS
+  if constexpr (FAST) {
+    // VR_FAST_COS 0 (parity ablation): the normal and the angle cosines in the exact variant's
+    // correctly rounded op sequence (the oracle's), only acos/pi as acospi_q and the opacity as
+    // exp2 differ from it
+    const float ginv = 1.f / sqrt_cr(dot3(g, g));
+    const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
+    const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
+    const float dli = dot3(li, n);
+    const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
+    float sq_in[3] = {dot3(n, n), dot3(li, li), dot3(lip, lip)}, sq[3];
+    sqrt_cr_n<3>(sq_in, sq);
+    const float nlen = sq[0], liplen = sq[2];
+    float alpha_n;
+    {
+      const float num[1] = {dot3(n, li)}, den[1] = {nlen * sq[1]};
+      float q[1];
+      div_acos_n<1>(num, den, q);
+      alpha_n = acospi_q(q[0]);
+    }
+    const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
+    for (int i = 0; i < P.num_lights; ++i) {
+      const DevLight L = P.lights[i];
+      const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
+      const float dlo = dot3(lo, n);
+      const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
+      float li_in[2] = {dot3(lo, lo), dot3(lop, lop)}, ln[2];
+      sqrt_cr_n<2>(li_in, ln);
+      const float num[2] = {dot3(n, lo), dot3(lip, lop)}, den[2] = {nlen * ln[0], liplen * ln[1]};
+      float q[2];
+      div_acos_n<2>(num, den, q);
+      const float rl = refl * lut_light<true>(P.lut, la, acospi_q(q[0]), acospi_q(q[1]));
+      ir = fmaf(rl * L.cr, P.color[0], ir);
+      ig = fmaf(rl * L.cg, P.color[1], ig);
+      ib = fmaf(rl * L.cb, P.color[2], ib);
+    }
+  } else
+#endif
   if constexpr (FAST) {
     // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
     const float ginv = __builtin_amdgcn_rsqf(dot3(g, g));

@@ -222,6 +222,13 @@ def render_device(handle, ra: VrRenderArgs, d_out: int, part=None, d_steps: int 
                                  ctypes.c_void_p(int(stream)) if stream else None))
 
 
+def last_march_kernel() -> str:
+    """The demangled name of the march kernel instantiation the last render launched."""
+    buf = ctypes.create_string_buffer(256)
+    check(lib().vr_last_march_kernel(buf, len(buf)))
+    return buf.value.decode()
+
+
 def assemble_partitions(d_parts: int, width: int, height: int, block_cols: int, num_parts: int, max_cols: int,
                         d_out: int, stream: int = 0) -> None:
     check(lib().vr_assemble_partitions(ctypes.c_void_p(int(d_parts)), int(width), int(height), int(block_cols),
