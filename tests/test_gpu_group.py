@@ -100,3 +100,78 @@ def test_group_render_device_on_a_stream(monkeypatch, counter_clock):
         assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))
     vr.volumeRender("delete", h)
     vr.volumeRender("delete", h1)
+
+
+def _ex3_channels(monkeypatch, devices, n=48, res=(90, 130)):
+    """Two example3.m-style channels (shell, and a second field with its own colour / factors), one
+    handle each (a group of `devices` when given)."""
+    if devices:
+        monkeypatch.setenv("VR_DEVICES", devices)
+    else:
+        monkeypatch.delenv("VR_DEVICES", raising=False)
+    lut = vr.Volume(vr.HenyeyGreenstein(32))
+    lut.TimeLastUpdate = np.uint64(7)
+    refl = vr.Volume(1)
+    refl.TimeLastUpdate = np.uint64(5)
+    R = np.flip(O.rotation(-15, 15, 15, R=O.rotation(90, 0, 0)), 0).astype(np.float32)
+    light = [vr.LightSource([-15, 15, 0], [0.5, 0.5, 0.5])]
+    data = [O.shell_volume(n), np.asfortranarray(O.shell_volume(n)[:, ::-1, :] * np.float32(0.5))]
+    chans = []
+    for i, (color, fe) in enumerate((([1, 1, 1], 1.0), ([0, 1, 0], 0.5))):
+        v = vr.Volume(data[i])
+        v.TimeLastUpdate = np.uint64(20 + i)
+        h = vr.volumeRender("new")
+        argv = (light, lut, np.float32([fe, 1, 1]), np.float32([1, 1, 1]), np.uint64(res), R,
+                np.float32([-0.03, 4.5, 6]), np.float32(0.95), np.float32(color))
+        chans.append((h, np.uint64(0), [v, refl, v], argv))
+    monkeypatch.delenv("VR_DEVICES", raising=False)
+    return chans
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0,0"])
+def test_group_fused_stereo_and_channels_equal_one_device(monkeypatch, counter_clock, devices):
+    """The fused commands on group handles: a stereo pair (vr_render_stereo) and a C4-style
+    two-channel stereo frame (vr_render_channels) rendered on a repeated-device group -- every device
+    its column part of every view, parts gathered and assembled per view -- equal one device bit for
+    bit, over two frames (the second after a data change of one channel)."""
+    monkeypatch.setenv("VR_GROUP_REPLICATE", "1")
+    out = {}
+    for name, devs in (("one", None), ("group", devices)):
+        chans = _ex3_channels(monkeypatch, devs)
+        frames = [mex.render_channels(chans, stereo=True, base=np.float32(0.03))]
+        v = chans[1][2][0]
+        v.Data = np.asfortranarray(v.Data * np.float32(1.5))
+        v.TimeLastUpdate = np.uint64(40)
+        frames.append(mex.render_channels(chans, stereo=True, base=np.float32(0.03)))
+        # the fused stereo pair of channel 0 alone (its handle re-synced)
+        h, t, vols, argv = chans[0]
+        vr.volumeRender("sync_volumes", h, t, *vols)
+        frames.append([vr.volumeRender("render_stereo", h, *argv, np.float32(0.03))])
+        out[name] = frames
+        for c in chans:
+            vr.volumeRender("delete", c[0])
+    for f1, f2 in zip(out["one"], out["group"]):
+        for pair1, pair2 in zip(f1, f2):
+            for a, b in zip(pair1, pair2):
+                assert a.max() > 0
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_group_mem_info_lists_every_device(monkeypatch, counter_clock):
+    """mem_info of a group handle: every device of the group, the replicas of the bound volumes it
+    holds and the last launch's kernel time on it (SURVEY.md s5 'Metrics')."""
+    import ctypes
+    from volume_renderer_amd import _lib
+    monkeypatch.setenv("VR_GROUP_REPLICATE", "1")
+    monkeypatch.setenv("VR_DEVICES", "0,0,0")
+    r = _scene(vr.VolumeRender(), vr.Volume(O.shell_volume(40)))
+    monkeypatch.delenv("VR_DEVICES")
+    r.render()
+    torch.cuda.synchronize()
+    buf = ctypes.create_string_buffer(1 << 16)
+    _lib.check(_lib.lib().vr_mem_info(mex._handle(r.objectHandle), buf, len(buf)))
+    txt = buf.value.decode()
+    assert txt.count("(primary)") == 1 and txt.count("(group member)") == 2, txt
+    assert txt.count("Emission:") == 3 and "(replica)" in txt, txt
+    assert "last launch (ms): n/a" not in txt, txt
+    r.delete()

@@ -186,6 +186,8 @@ struct DevBuf {
   // completions of the launches / peer copies that read it (vr_resources.h): it is neither
   // rewritten nor freed before all of them
   vr_host::Readers readers;
+  // a replica: completion of the peer copy that fills it (a launch on any stream waits for it)
+  vr_host::EventPtr ready;
   // multi-device group (vr_new_multi): its copies on the other devices, and the version each copies
   std::map<int, std::shared_ptr<DevBuf>> replicas;
   std::map<int, uint64_t> replica_of;
@@ -238,6 +240,10 @@ struct vr_context {
   hipEvent_t gdone = nullptr;     // child: its part has landed on the primary
   float *d_part = nullptr;        // child: its part image; primary: all parts
   size_t d_part_bytes = 0;
+  // the last launch's kernel time on this context's device (events around the march launch of
+  // do_render / a fused channel launch), reported by mem_info; created on first use
+  hipEvent_t tev[2] = {nullptr, nullptr};
+  bool timed = false;
 };
 
 namespace {
@@ -689,9 +695,15 @@ void upload_lights(vr_context *h, const vr_render_args *a) {
 // gradient) is marked with the launch's completion event by finish(); the frame's light list is
 // staged on the launch stream.
 using LaunchRec = vr_host::LaunchRec<BufPtr>;
+void wait_ready(const BufPtr &b, hipStream_t s) {  // a replica's peer copy, possibly on another stream
+  if (b && !vr_host::done(b->ready)) VR_HIP(hipStreamWaitEvent(s, b->ready->e, 0));
+}
 void bind_reads(LaunchRec &L) {
   for (const BufPtr &b : g_tex.bind)
-    if (b) L.reads.push_back(b);
+    if (b) {
+      wait_ready(b, L.stream);
+      L.reads.push_back(b);
+    }
   for (const auto &kv : g_tex.gvec)
     if (kv.second.buf && kv.first == L.device) L.reads.push_back(kv.second.buf);
 }
@@ -932,6 +944,18 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   return hipSuccess;
 }
 
+// Launch timing for mem_info (the context's device must be current).
+void time_mark(vr_context *h, int which, hipStream_t stream) {
+  if (!h->tev[0]) {
+    if (hipEventCreate(&h->tev[0]) != hipSuccess || hipEventCreate(&h->tev[1]) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+  }
+  if (hipEventRecord(h->tev[which], stream) != hipSuccess) (void)hipGetLastError();
+  if (which == 1) h->timed = true;
+}
+
 int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, float *d_out,
               unsigned long long *d_steps, hipStream_t stream, Frame &F, float *d_out2 = nullptr,
               const float *eye2 = nullptr, int *fusable = nullptr) {
@@ -1000,6 +1024,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       gv->device = h->device;
       gv->bytes = n * 4 * sizeof(float);
       if (vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device) == hipSuccess) {
+        for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);
         VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
         G.buf = gv;
         for (int i = 0; i < 3; ++i) {
@@ -1041,7 +1066,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
                                         VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
       P.view_blocks = vfns[ki](P);
     }
+    time_mark(h, 0, stream);
     VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
+    time_mark(h, 1, stream);
     if (F.sched_copy) {  // a timed full frame: its block durations to the host, for the tail test
       vr_context::Schedule &S = *F.sched_copy;
       VR_HIP(hipMemcpyAsync(S.h_cost, S.d_cost, (size_t)S.blocks * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1181,6 +1208,7 @@ BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
     VR_HIP(vr_host::record_event(s, ev));
     b->readers.add(ev);
     r->readers.add(ev);
+    r->ready = ev;
   }
   for (int i = 0; i < 3; ++i) r->dims[i] = b->dims[i];
   r->nonfinite = b->nonfinite;
@@ -1215,12 +1243,70 @@ void group_sync(vr_context *h) {
   }
 }
 
+// Part buffers of a group frame of `nviews` images: the primary's h->d_part holds every device's
+// parts view-major (view v, device k at (v * n + k) * part_floats: one view's parts are contiguous,
+// as vr_assemble_partitions reads them); a child's d_part its own nviews parts.
+void ensure_part_buffers(vr_context *h, int n, size_t part_floats, int nviews) {
+  const size_t pb = (size_t)n * (size_t)nviews * part_floats * sizeof(float);
+  if (h->d_part_bytes < pb) {
+    if (h->d_part) VR_HIP(hipFree(h->d_part));
+    h->d_part = nullptr;
+    h->d_part_bytes = 0;
+    VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&h->d_part), pb));
+    h->d_part_bytes = pb;
+  }
+  for (vr_context *c : h->children) {
+    DeviceGuard dg(c->device);
+    const size_t cb = (size_t)nviews * part_floats * sizeof(float);
+    if (c->d_part_bytes < cb) {
+      if (c->d_part) VR_HIP(hipFree(c->d_part));
+      c->d_part = nullptr;
+      c->d_part_bytes = 0;
+      VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&c->d_part), cb));
+      c->d_part_bytes = cb;
+    }
+  }
+}
+
+// Bind, for a render on child c, the replicas of the primary's bindings `saved` on c's device (the
+// LUT is c's own upload, which do_render keeps resident).
+void bind_replicas(vr_context *h, vr_context *c, const BufPtr (&saved)[T_COUNT]) {
+  for (int t = 0; t < T_COUNT; ++t) c->vol[t] = h->vol[t];
+  for (int t = 0; t < T_COUNT; ++t)
+    g_tex.bind[t] = t == T_LIGHT ? c->buf[T_LIGHT] : replicate(saved[t], c->device, c->gstream);
+}
+
+// Gather every child's parts (nviews images each) into the primary's part buffer over xGMI and
+// assemble each view into d_outs[v] on the primary's `stream`.
+void group_gather_assemble(vr_context *h, int nviews, size_t part_floats, int64_t W, int64_t H, int32_t bc,
+                           int64_t maxc, float *const *d_outs, hipStream_t stream) {
+  const int n = 1 + (int)h->children.size();
+  for (int k = 1; k < n; ++k) {
+    vr_context *c = h->children[k - 1];
+    DeviceGuard dg(c->device);
+    // the previous frame's assembly has read these slots of the primary's part buffer
+    VR_HIP(hipStreamWaitEvent(c->gstream, h->gdone, 0));
+    for (int v = 0; v < nviews; ++v)
+      VR_HIP(hipMemcpyPeerAsync(h->d_part + ((size_t)v * n + k) * part_floats, h->device,
+                                c->d_part + (size_t)v * part_floats, c->device, part_floats * sizeof(float),
+                                c->gstream));
+    VR_HIP(hipEventRecord(c->gdone, c->gstream));
+  }
+  for (vr_context *c : h->children) VR_HIP(hipStreamWaitEvent(stream, c->gdone, 0));
+  for (int v = 0; v < nviews; ++v)
+    VR_HIP(vr::launch_assemble(h->d_part + (size_t)v * n * part_floats, W, H, bc, n, maxc, d_outs[v], stream));
+  VR_HIP(hipEventRecord(h->gdone, stream));
+}
+
 // 'render' on a group: child k renders column part k (16-column blocks dealt round-robin, as
 // bench.py's ranks), the primary part 0; the children's parts are peer-copied into the primary's
-// part buffer and assembled there into d_out (the primary's device, on `stream`).  The module-global
-// bindings are the primary's again when this returns.
-int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream_t stream) {
+// part buffer and assembled there into d_out (the primary's device, on `stream`).  With d_out2 /
+// eye2 every device renders its part of both eyes of a stereo pair (vr_render_stereo) in one launch.
+// The module-global bindings are the primary's again when this returns.
+int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream_t stream, float *d_out2 = nullptr,
+                 const float *eye2 = nullptr) {
   const int n = 1 + (int)h->children.size();
+  const int nviews = d_out2 ? 2 : 1;
   const int32_t bc = 16;
   const int64_t W = (int64_t)a->resolution[1], H = (int64_t)a->resolution[0];
   vr_partition p0{bc, 0, n, 0};
@@ -1228,51 +1314,30 @@ int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream
   const size_t part_floats = (size_t)maxc * (size_t)H * 3;
   if (!part_floats) {
     Frame F;
-    return do_render(h, a, nullptr, d_out, nullptr, stream, F);
+    return do_render(h, a, nullptr, d_out, nullptr, stream, F, d_out2, eye2);
   }
-  if (h->d_part_bytes < (size_t)n * part_floats * sizeof(float)) {
-    if (h->d_part) VR_HIP(hipFree(h->d_part));
-    h->d_part = nullptr;
-    h->d_part_bytes = 0;
-    VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&h->d_part), (size_t)n * part_floats * sizeof(float)));
-    h->d_part_bytes = (size_t)n * part_floats * sizeof(float);
-  }
-  // the primary's part first: it uploads the frame's lights / LUT and binds them.  Slot 0 of the
-  // part buffer is read by the previous frame's assembly, which may run on another stream.
+  ensure_part_buffers(h, n, part_floats, nviews);
+  // the primary's part first: it uploads the frame's lights / LUT and binds them.  Its slots of the
+  // part buffer are read by the previous frame's assembly, which may run on another stream.
   VR_HIP(hipStreamWaitEvent(stream, h->gdone, 0));
   Frame F0;
-  int rc = do_render(h, a, &p0, h->d_part, nullptr, stream, F0);
+  int rc = do_render(h, a, &p0, h->d_part, nullptr, stream, F0, d_out2 ? h->d_part + (size_t)n * part_floats : nullptr,
+                     eye2);
   if (rc) return rc;
   BufPtr saved[T_COUNT];
   for (int t = 0; t < T_COUNT; ++t) saved[t] = g_tex.bind[t];
-  for (int k = 1; k < n; ++k) {
+  for (int k = 1; k < n && !rc; ++k) {
     vr_context *c = h->children[k - 1];
     DeviceGuard dg(c->device);
-    if (c->d_part_bytes < part_floats * sizeof(float)) {
-      if (c->d_part) VR_HIP(hipFree(c->d_part));
-      c->d_part = nullptr;
-      c->d_part_bytes = 0;
-      VR_HIP(vr_host::device_alloc(reinterpret_cast<void **>(&c->d_part), part_floats * sizeof(float)));
-      c->d_part_bytes = part_floats * sizeof(float);
-    }
-    for (int t = 0; t < T_COUNT; ++t) c->vol[t] = h->vol[t];
-    for (int t = 0; t < T_COUNT; ++t)  // the LUT: the child's own upload (do_render keeps it resident)
-      g_tex.bind[t] = t == T_LIGHT ? c->buf[T_LIGHT] : replicate(saved[t], c->device, c->gstream);
+    bind_replicas(h, c, saved);
     vr_partition pk{bc, k, n, 0};
     Frame F;
-    rc = do_render(c, a, &pk, c->d_part, nullptr, c->gstream, F);
-    if (rc) break;
-    // the previous frame's assembly has read this slot of the primary's part buffer
-    VR_HIP(hipStreamWaitEvent(c->gstream, h->gdone, 0));
-    VR_HIP(hipMemcpyPeerAsync(h->d_part + (size_t)k * part_floats, h->device, c->d_part, c->device,
-                              part_floats * sizeof(float), c->gstream));
-    VR_HIP(hipEventRecord(c->gdone, c->gstream));
+    rc = do_render(c, a, &pk, c->d_part, nullptr, c->gstream, F, d_out2 ? c->d_part + part_floats : nullptr, eye2);
   }
   for (int t = 0; t < T_COUNT; ++t) g_tex.bind[t] = saved[t];
   if (rc) return rc;
-  for (vr_context *c : h->children) VR_HIP(hipStreamWaitEvent(stream, c->gdone, 0));
-  VR_HIP(vr::launch_assemble(h->d_part, W, H, bc, n, maxc, d_out, stream));
-  VR_HIP(hipEventRecord(h->gdone, stream));
+  float *outs[2] = {d_out, d_out2};
+  group_gather_assemble(h, nviews, part_floats, W, H, bc, maxc, outs, stream);
   return VR_OK;
 }
 
@@ -1286,6 +1351,8 @@ void delete_children(vr_context *h) {
     free_schedules(c);
     free_views(c);
     if (c->gdone) (void)hipEventDestroy(c->gdone);
+    for (hipEvent_t e : c->tev)
+      if (e) (void)hipEventDestroy(e);
     if (c->gstream) (void)hipStreamDestroy(c->gstream);
     delete c;
   }
@@ -1431,6 +1498,8 @@ int vr_delete(vr_context *h) {
   }
   delete_children(h);
   if (h->gdone) (void)hipEventDestroy(h->gdone);
+  for (hipEvent_t e : h->tev)
+    if (e) (void)hipEventDestroy(e);
   if (h->d_part) (void)hipFree(h->d_part);
   g_contexts.erase(h);
   h->signature = 0;
@@ -1477,6 +1546,44 @@ int vr_mem_info(vr_context *h, char *buf, size_t buflen) {
      << "\t\tSlots (emission/absorption/reflection): " << g_tex.idx_em << " " << g_tex.idx_ab << " "
      << g_tex.idx_re << ", gradient method: " << (g_tex.grad_method == G_LOOKUP ? "lookup" : "compute")
      << ", lights: " << g_tex.lights.size() << "\n";
+  // per-device residency and the last launch's kernel time (SURVEY.md s5 "Metrics"): the primary
+  // and, for a group (vr_new_multi), every child with the replicas of the bound volumes it holds
+  os << "\n\tDevices\n\t-------\n";
+  static const char *const tex_names[T_COUNT] = {"Emission", "Absorption", "Reflection", "dX", "dY", "dZ", "light"};
+  std::vector<vr_context *> ctxs{h};
+  ctxs.insert(ctxs.end(), h->children.begin(), h->children.end());
+  for (size_t k = 0; k < ctxs.size(); ++k) {
+    vr_context *c = ctxs[k];
+    DeviceGuard dk(c->device);
+    size_t fb = 0, tb = 0;
+    VR_HIP(hipMemGetInfo(&fb, &tb));
+    os << "\t\tdevice " << c->device << (k == 0 ? " (primary)" : " (group member)") << ": used (MB) "
+       << mb(tb - fb) << " of " << mb(tb) << ", part buffer (MB) " << mb(c->d_part_bytes)
+       << ", reusable buffers (MB) " << mb(vr_host::pool_bytes(c->device)) << "\n";
+    for (int t = 0; t < T_COUNT; ++t) {
+      const BufPtr &b = g_tex.bind[t];
+      if (!b) continue;
+      const DevBuf *r = nullptr;
+      if (k == 0) {
+        r = b.get();
+      } else if (t == T_LIGHT) {
+        r = c->buf[T_LIGHT].get();
+      } else {
+        auto it = b->replicas.find(c->device);
+        if (b->device == c->device && it == b->replicas.end()) r = b.get();
+        else if (it != b->replicas.end() && b->replica_of[c->device] == b->version) r = it->second.get();
+      }
+      os << "\t\t\t" << tex_names[t] << ": ";
+      if (r) os << mb(r->bytes) << " MB resident at " << (const void *)r->ptr << (k && t != T_LIGHT ? " (replica)" : "") << "\n";
+      else os << "not resident (replicated at the next render)\n";
+    }
+    float ms = -1.f;
+    if (c->timed && hipEventQuery(c->tev[1]) == hipSuccess && hipEventElapsedTime(&ms, c->tev[0], c->tev[1]) == hipSuccess)
+      os << "\t\t\tlast launch (ms): " << ms << "\n";
+    else
+      os << "\t\t\tlast launch (ms): n/a\n";
+    (void)hipGetLastError();
+  }
   const std::string s = os.str();
   if (buf && buflen) {
     const size_t n = std::min(buflen - 1, s.size());
@@ -1560,6 +1667,80 @@ int vr_sync_volumes(vr_context *h, uint64_t time_last_mem_sync, const vr_volume 
 // aliasing, slot size, shading) group, their views' parameters in device memory.  The buffers a
 // prepared frame reads stay referenced until the call returns; a later channel's sync never
 // overwrites them (each handle owns its buffers).
+// The fusable views one device collects for its march_views launches.
+struct ViewSet {
+  std::vector<BufPtr> keep;
+  std::vector<vr::RenderParams> views;
+  std::vector<std::array<double, 3>> drift;
+  std::vector<int> vmode, vab;
+  std::vector<vr::DevLight> lights;
+  std::vector<size_t> loff;
+};
+
+// Launch the collected views of one device on `stream` (the device current): one march_views launch
+// per (gradient mode, absorption aliasing, slot size, shading) group, in channel order within a group.
+void launch_view_set(ViewSet &VS, int device, hipStream_t stream, vr_context *timer) {
+  if (VS.views.empty()) return;
+  std::vector<vr::RenderParams> &views = VS.views;
+  const size_t nvw = views.size();
+  std::vector<size_t> order(nvw);
+  for (size_t k = 0; k < nvw; ++k) order[k] = k;
+  auto key = [&](size_t k) {
+    return ((VS.vmode[k] * 2 + VS.vab[k]) * 2 + views[k].wide_slot) * 2 + views[k].fast_shade;
+  };
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return key(x) < key(y); });
+  // the views' lights, staged for these launches on their stream (each channel's own list)
+  LaunchRec L;
+  L.stream = stream;
+  L.device = device;
+  L.reads = std::move(VS.keep);
+  for (const BufPtr &b : L.reads) wait_ready(b, stream);
+  const void *dl = nullptr;
+  VR_HIP(L.stage(VS.lights.data(), VS.lights.size() * sizeof(vr::DevLight), &dl));
+  const vr::DevLight *d_lights = static_cast<const vr::DevLight *>(dl);
+  typedef hipError_t (*views_fn)(const vr::RenderViews &, uint32_t, int, bool, hipStream_t);
+  static const views_fn vfns[2][3] = {
+      {vr::exact::launch_march_views_k1, vr::exact::launch_march_views_k2, vr::exact::launch_march_views_k4},
+      {vr::fast::launch_march_views_k1, vr::fast::launch_march_views_k2, vr::fast::launch_march_views_k4}};
+  time_mark(timer, 0, stream);
+  size_t g0 = 0;
+  while (g0 < nvw) {
+    size_t g1 = g0;
+    while (g1 < nvw && key(order[g1]) == key(order[g0])) ++g1;
+    // depth lanes as for one view: the frame's own tail sets them, and K = 2 stays ahead of K = 1
+    // per sample even at many waves per slot (DESIGN.md s5)
+    const int K = std::min(depth_lanes(views[order[g0]]), 4);
+    vr::RenderViews V;
+    std::memset(&V, 0, sizeof V);
+    for (size_t k = g0; k < g1; ++k) {
+      vr::RenderParams &P = V.p[k - g0];
+      P = views[order[k]];
+      for (int d = 0; d < 3; ++d) P.tap_off[d] += (float)(chunk_samples(K) * VS.drift[order[k]][d]);
+      P.lights = d_lights ? d_lights + VS.loff[order[k]] : nullptr;
+    }
+    const size_t v0 = order[g0];
+    VR_HIP(vfns[views[v0].fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](V, (uint32_t)(g1 - g0), VS.vmode[v0],
+                                                                              VS.vab[v0] != 0, stream));
+    g0 = g1;
+  }
+  time_mark(timer, 1, stream);
+  // a prepared frame's buffer that no handle or binding holds any more is freed when these launches
+  // complete (vr_host::free_when_done); the launches stay asynchronous
+  VR_HIP(L.finish());
+}
+
+// Multi-channel render (vr_render_channels): channel i is what vr_sync_volumes +
+// vr_render (or vr_render_stereo) on ch[i] would produce were it the only object -- before its
+// sync the texture bindings its handle's last sync left are restored (the reference's textures are
+// module globals: with one object per channel an unchanged channel would otherwise render the
+// previous channel's volumes); the syncs run in channel order, each channel's frame is prepared
+// against the textures its own sync bound, and the frames the staged march can take are marched
+// together in one launch per (gradient mode, absorption aliasing, slot size, shading) group, their
+// views' parameters in kernel arguments.  The buffers a prepared frame reads stay referenced until
+// its launch completes; a later channel's sync never overwrites them (each handle owns its buffers).
+// Group handles (vr_new_multi, all channels on the same devices): every device renders its column
+// part of every view (the channel's bindings replicated to it, as group_render does), the parts are
+// gathered to the primary of channel 0 over xGMI and assembled there, view by view.
 static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, float base, float *d_out,
                               hipStream_t stream) {
   if (!ch || n < 1) return fail(VR_ERR_ARGUMENT, "no channels");
@@ -1573,16 +1754,34 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
     if (ch[i].args->resolution[0] != ch[0].args->resolution[0] || ch[i].args->resolution[1] != ch[0].args->resolution[1])
       return fail(VR_ERR_ARGUMENT, "channels differ in image resolution");
     if (ch[i].handle->device != ch[0].handle->device) return fail(VR_ERR_ARGUMENT, "channels on different devices");
+    if (ch[i].handle->children.size() != ch[0].handle->children.size())
+      return fail(VR_ERR_ARGUMENT, "channels on different device groups");
+    for (size_t k = 0; k < ch[i].handle->children.size(); ++k)
+      if (ch[i].handle->children[k]->device != ch[0].handle->children[k]->device)
+        return fail(VR_ERR_ARGUMENT, "channels on different device groups");
   }
   const size_t img = (size_t)ch[0].args->resolution[0] * (size_t)ch[0].args->resolution[1] * 3;
   if (img && !d_out) return fail(VR_ERR_ARGUMENT, "output is NULL");
   const bool fuse = !env_flag("VR_NO_FUSED_CHANNELS");
-  std::vector<BufPtr> keep;
-  std::vector<vr::RenderParams> views;
-  std::vector<std::array<double, 3>> drift;
-  std::vector<int> vmode, vab;
-  std::vector<vr::DevLight> lights;
-  std::vector<size_t> loff;
+  vr_context *h0 = ch[0].handle;
+  const int ndev = 1 + (int)h0->children.size();
+  const int32_t bc = 16;
+  const int64_t W = (int64_t)ch[0].args->resolution[1], H = (int64_t)ch[0].args->resolution[0];
+  const int64_t maxc = part_columns(W, bc, 0, ndev);
+  const size_t part_floats = (size_t)maxc * (size_t)H * 3;
+  const bool grouped = ndev > 1 && part_floats > 0;
+  const int nviews = n * nv;  // view vi = i * nv + e
+  if (grouped) {
+    ensure_part_buffers(h0, ndev, part_floats, nviews);
+    VR_HIP(hipStreamWaitEvent(stream, h0->gdone, 0));  // the previous frame's assembly read part 0
+  }
+  // where view vi of device k goes: the caller's image (one device) or the part buffers
+  auto out_of = [&](int k, int vi) -> float * {
+    if (!grouped) return d_out + (size_t)vi * img;
+    if (k == 0) return h0->d_part + ((size_t)vi * ndev) * part_floats;
+    return h0->children[k - 1]->d_part + (size_t)vi * part_floats;
+  };
+  std::vector<ViewSet> sets(grouped ? ndev : 1);
   for (int i = 0; i < n; ++i) {
     vr_context *h = ch[i].handle;
     if (h->has_snap) {  // this channel's own bindings, not the previous channel's
@@ -1595,6 +1794,7 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
     int rc = do_sync_volumes(h, ch[i].time_last_mem_sync, ch[i].emission, ch[i].reflection, ch[i].absorption,
                              ch[i].dx, ch[i].dy, ch[i].dz);
     if (rc) return rc;
+    if (grouped) group_sync(h);
     vr_render_args a = *ch[i].args;
     float eye2[3] = {0.f, 0.f, 0.f};
     if (stereo) {  // as vr_render_stereo: left = the frame's eye at -base, right at +base
@@ -1603,74 +1803,52 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
       const float X[3] = {r[2], r[1], r[0]}, Z[3] = {r[8], r[7], r[6]};
       for (int k = 0; k < 3; ++k) eye2[k] = fmaf(-a.props[2], Z[k], base * X[k]);
     }
-    float *dl = d_out + (size_t)i * nv * img, *dr = stereo ? dl + img : nullptr;
-    Frame F;
-    int fz = 0;
-    rc = do_render(h, &a, nullptr, dl, nullptr, stream, F, dr, stereo ? eye2 : nullptr, fuse ? &fz : nullptr);
+    BufPtr saved[T_COUNT];
+    for (int t = 0; t < T_COUNT; ++t) saved[t] = g_tex.bind[t];
+    for (int k = 0; k < (grouped ? ndev : 1) && !rc; ++k) {
+      vr_context *ctx = k == 0 ? h : h->children[k - 1];
+      DeviceGuard dg(ctx->device);
+      hipStream_t s = k == 0 ? stream : h0->children[k - 1]->gstream;
+      if (k > 0) bind_replicas(h, ctx, saved);
+      vr_partition pk{bc, k, ndev, 0};
+      float *dl = out_of(k, i * nv), *dr = stereo ? out_of(k, i * nv + 1) : nullptr;
+      Frame F;
+      int fz = 0;
+      rc = do_render(ctx, &a, grouped ? &pk : nullptr, dl, nullptr, s, F, dr, stereo ? eye2 : nullptr,
+                     fuse ? &fz : nullptr);
+      if (rc || !fz) continue;  // (rendered by its own launch against the textures bound now)
+      ViewSet &VS = sets[k];
+      for (const BufPtr &b : g_tex.bind)
+        if (b) VS.keep.push_back(b);
+      for (int v = 0; v < nv; ++v) {
+        vr::RenderParams P = F.P;
+        P.views = 1;
+        P.out2 = nullptr;
+        P.view_blocks = 0;
+        P.out = v ? dr : dl;
+        if (v)
+          for (int d = 0; d < 3; ++d) P.eye[d] = eye2[d];
+        VS.views.push_back(P);
+        VS.drift.push_back({F.drift1[0], F.drift1[1], F.drift1[2]});
+        VS.vmode.push_back(F.mode);
+        VS.vab.push_back(F.ab_alias ? 1 : 0);
+        VS.loff.push_back(VS.lights.size());
+      }
+      VS.lights.insert(VS.lights.end(), g_tex.lights.begin(), g_tex.lights.end());
+    }
+    for (int t = 0; t < T_COUNT; ++t) g_tex.bind[t] = saved[t];
     if (rc) return rc;
-    if (!fz) continue;  // rendered by its own launch against the textures bound now
-    for (const BufPtr &b : g_tex.bind)
-      if (b) keep.push_back(b);
-    for (int v = 0; v < nv; ++v) {
-      vr::RenderParams P = F.P;
-      P.views = 1;
-      P.out2 = nullptr;
-      P.view_blocks = 0;
-      P.out = v ? dr : dl;
-      if (v)
-        for (int k = 0; k < 3; ++k) P.eye[k] = eye2[k];
-      views.push_back(P);
-      drift.push_back({F.drift1[0], F.drift1[1], F.drift1[2]});
-      vmode.push_back(F.mode);
-      vab.push_back(F.ab_alias ? 1 : 0);
-      loff.push_back(lights.size());
-    }
-    lights.insert(lights.end(), g_tex.lights.begin(), g_tex.lights.end());
   }
-  if (views.empty()) return VR_OK;
-  // group the views by launch variant (contiguous in device memory), in channel order within a group
-  const size_t nvw = views.size();
-  std::vector<size_t> order(nvw);
-  for (size_t k = 0; k < nvw; ++k) order[k] = k;
-  auto key = [&](size_t k) {
-    return ((vmode[k] * 2 + vab[k]) * 2 + views[k].wide_slot) * 2 + views[k].fast_shade;
-  };
-  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return key(x) < key(y); });
-  // the views' lights, staged for these launches on their stream (each channel's own list)
-  LaunchRec L;
-  L.stream = stream;
-  L.device = ch[0].handle->device;
-  L.reads = std::move(keep);
-  const void *dl = nullptr;
-  VR_HIP(L.stage(lights.data(), lights.size() * sizeof(vr::DevLight), &dl));
-  const vr::DevLight *d_lights = static_cast<const vr::DevLight *>(dl);
-  typedef hipError_t (*views_fn)(const vr::RenderViews &, uint32_t, int, bool, hipStream_t);
-  static const views_fn vfns[2][3] = {
-      {vr::exact::launch_march_views_k1, vr::exact::launch_march_views_k2, vr::exact::launch_march_views_k4},
-      {vr::fast::launch_march_views_k1, vr::fast::launch_march_views_k2, vr::fast::launch_march_views_k4}};
-  size_t g0 = 0;
-  while (g0 < nvw) {
-    size_t g1 = g0;
-    while (g1 < nvw && key(order[g1]) == key(order[g0])) ++g1;
-    // depth lanes as for one view: the frame's own tail sets them, and K = 2 stays ahead of K = 1
-    // per sample even at many waves per slot (DESIGN.md s5)
-    const int K = std::min(depth_lanes(views[order[g0]]), 4);
-    vr::RenderViews V;
-    std::memset(&V, 0, sizeof V);
-    for (size_t k = g0; k < g1; ++k) {
-      vr::RenderParams &P = V.p[k - g0];
-      P = views[order[k]];
-      for (int d = 0; d < 3; ++d) P.tap_off[d] += (float)(chunk_samples(K) * drift[order[k]][d]);
-      P.lights = d_lights ? d_lights + loff[order[k]] : nullptr;
-    }
-    const size_t v0 = order[g0];
-    VR_HIP(vfns[views[v0].fast_shade ? 1 : 0][K == 1 ? 0 : (K == 2 ? 1 : 2)](V, (uint32_t)(g1 - g0), vmode[v0],
-                                                                              vab[v0] != 0, stream));
-    g0 = g1;
+  for (int k = 0; k < (int)sets.size(); ++k) {
+    vr_context *ctx = k == 0 ? h0 : h0->children[k - 1];
+    DeviceGuard dg(ctx->device);
+    launch_view_set(sets[k], ctx->device, k == 0 ? stream : ctx->gstream, ctx);
   }
-  // a prepared frame's buffer that no handle or binding holds any more is freed when these launches
-  // complete (vr_host::free_when_done); the launches stay asynchronous
-  VR_HIP(L.finish());
+  if (grouped) {
+    std::vector<float *> outs(nviews);
+    for (int vi = 0; vi < nviews; ++vi) outs[vi] = d_out + (size_t)vi * img;
+    group_gather_assemble(h0, nviews, part_floats, W, H, bc, maxc, outs.data(), stream);
+  }
   return VR_OK;
 }
 
@@ -1771,7 +1949,8 @@ int vr_render_stereo(vr_context *h, const vr_render_args *a, float base, float *
   for (int i = 0; i < 3; ++i) eye2[i] = fmaf(-dist, Z[i], base * X[i]);
   Frame F;
   float *d_left = h->d_out, *d_right = h->d_out + bytes / sizeof(float);
-  int rc = do_render(h, &al, nullptr, d_left, nullptr, nullptr, F, d_right, eye2);
+  int rc = h->children.empty() ? do_render(h, &al, nullptr, d_left, nullptr, nullptr, F, d_right, eye2)
+                               : group_render(h, &al, d_left, nullptr, d_right, eye2);  // every device
   if (rc) return rc;
   if (bytes) {
     VR_HIP(hipMemcpy(out_left, d_left, bytes, hipMemcpyDeviceToHost));
