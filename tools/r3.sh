@@ -4,7 +4,8 @@
 # (with variants) the full-size shading ablation.  Outputs under gpurun_out/RUN.
 RUN=${1:-r3}; shift
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$RUN &&
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/$RUN/tests.log 2>&1 &&
+{ timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > gpurun_out/$RUN/tests.log 2>&1;
+  rc=$?; echo "pytest rc=$rc" >> gpurun_out/$RUN/tests.log; [ $rc -le 1 ]; } &&
 timeout -k 10 400 python bench.py > gpurun_out/$RUN/bench.json 2> gpurun_out/$RUN/bench.err &&
 (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$RUN/kt -o kt --output-format csv -- \

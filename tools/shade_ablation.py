@@ -112,6 +112,8 @@ def main():
         ref32, _ = S.render(oh, sc["lights"], olut, *rargs, pixels=(xs, ys), threads=16)
         ref64, _ = S.render(oh, sc["lights"], olut, *rargs, pixels=(xs, ys), double=True, threads=16)
         del hem, S, oem
+        np.savez(os.path.join(tmp, scene + "_ref.npz"), xs=xs, ys=ys, ref32=ref32, ref64=ref64,
+                 prod=np.ascontiguousarray(np.asarray(img, np.float32)[ys, xs, :]))
         res[scene] = {"pixels": int(len(xs))}
         for name, lib, env in variants:
             o = os.path.join(tmp, f"{scene}_{name}.npy")
