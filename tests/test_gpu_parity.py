@@ -584,7 +584,9 @@ def test_fused_stereo_equals_two_renders(monkeypatch, counter_clock, lit):
     monkeypatch.setenv("VR_NO_FUSED_STEREO", "1")
     two = r.render()
     monkeypatch.delenv("VR_NO_FUSED_STEREO")
+    monkeypatch.setenv("VR_FUSED_STEREO", "1")
     fused = r.render()
+    monkeypatch.delenv("VR_FUSED_STEREO")
     assert two.max() > 0 and two.shape == fused.shape
     assert np.array_equal(np.asarray(two, np.float32).view(np.uint32), np.asarray(fused, np.float32).view(np.uint32))
     r.delete()
