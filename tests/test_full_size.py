@@ -35,6 +35,9 @@ torch = pytest.importorskip("torch")
 from volume_renderer_amd import mex  # noqa: E402
 
 THREADS = 16  # the GPU box's CPU share (os.cpu_count() there reports the whole host)
+# the product may be at most half as far from the fp32 oracle (RMS over lit sampled channels) as the
+# fp32 oracle is from exact arithmetic (fp64), at every full-size config, default shading included
+MAX_RMS_RATIO = 0.5
 EX1_LIGHTS = np.array([[500, 1000, 550, 0, 1, 1], [0, 550, 90, 1, 0.5, 1]], np.float32)
 EX3_LIGHT = np.array([[-15, 15, 0, 0.5, 0.5, 0.5]], np.float32)
 
@@ -139,8 +142,9 @@ def oracle_check(S, h, lights, lut, rargs, img, R, props, bmax, what, seed=1):
     ref32, st32 = S.render(h, lights, lut, *rargs, pixels=(xs, ys), threads=THREADS)
     ref64, _ = S.render(h, lights, lut, *rargs, pixels=(xs, ys), double=True, threads=THREADS)
     got = np.ascontiguousarray(np.asarray(img, np.float32)[ys, xs, :])
-    stats = assert_parity_full_size(got, ref32, ref64, what)
-    u = assert_parity_full_size(got[uni], ref32[uni], ref64[uni], what + " (uniform pixels)")
+    stats = assert_parity_full_size(got, ref32, ref64, what, max_rms_ratio=MAX_RMS_RATIO)
+    u = assert_parity_full_size(got[uni], ref32[uni], ref64[uni], what + " (uniform pixels)",
+                                max_rms_ratio=MAX_RMS_RATIO)
     stats.update(pixels=int(len(xs)), uniform_pixels=int(uni.sum()), samples=int(st32.sum()),
                  lit_pixels=float((ref32.max(axis=1) > 0).mean()), uniform_frac_within_survey=u["frac_within_survey"],
                  uniform_rms_ratio=u["rms_ratio"])
@@ -204,21 +208,26 @@ def partition_check(sc, nparts, bc=16, want_k=None):
         assert np.array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32)), (nparts, launch)
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("shade", ["fast", "exact"])
-def test_c2_1024x768_compute_gradient(monkeypatch, shade):
-    """C2 with the default (fast) shading arithmetic, and with VR_EXACT_SHADE=1 (the oracle's op
-    sequence)."""
-    if shade == "exact":
-        monkeypatch.setenv("VR_EXACT_SHADE", "1")
-    else:
-        monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
-    sc = ex1_scene(1024, 1024, 768)
-    st = oracle_check(sc["S"], sc["oh"], EX1_LIGHTS, sc["olut"], sc["rargs"], sc["img"], sc["R"], [0, 3, 6],
-                      (1, 1, 1), f"C2 V_shell(1024) 1024x768 {shade}")
-    if shade == "exact":  # only acosf / expf come from another library: much closer than fp32 rounding
-        assert st["rms_ratio"] <= 0.25, st
-    vr.volumeRender("delete", sc["h"])
+@pytest.mark.timeout(400)
+def test_c2_1024x768_compute_gradient(monkeypatch):
+    """C2 with VR_EXACT_SHADE=1 (the oracle's op sequence) and with the default (fast)
+    shading arithmetic.  The unfloored SURVEY.md 8c fraction of the default shading may fall at
+    most 0.5 percentage points below the exact-op kernel's own (so the floored envelope of
+    assert_parity_full_size cannot hide a regression of the default arithmetic)."""
+    st = {}
+    for shade in ("exact", "fast"):
+        if shade == "exact":
+            monkeypatch.setenv("VR_EXACT_SHADE", "1")
+        else:
+            monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
+        sc = ex1_scene(1024, 1024, 768)
+        st[shade] = oracle_check(sc["S"], sc["oh"], EX1_LIGHTS, sc["olut"], sc["rargs"], sc["img"], sc["R"], [0, 3, 6],
+                                 (1, 1, 1), f"C2 V_shell(1024) 1024x768 {shade}")
+        vr.volumeRender("delete", sc["h"])
+        del sc
+    # only acosf comes from another library in the exact kernel: much closer than fp32 rounding
+    assert st["exact"]["rms_ratio"] <= 0.25, st["exact"]
+    assert st["fast"]["frac_within_survey"] >= st["exact"]["frac_within_survey"] - 0.005, st
 
 
 @pytest.mark.timeout(300)

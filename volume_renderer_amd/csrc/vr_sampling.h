@@ -416,16 +416,36 @@ __device__ __forceinline__ float acospi_q(float q) {
 #endif
 }
 
-// 1 - __expf(-a * dx) (volumeRender_kernel.cu:456).  Exact variant: the correctly rounded-ish
-// device expf the oracle models; fast variant: what __expf is, exp2 of x * log2(e) on the
-// hardware exp unit (v_exp_f32).
+// exp(-x) rounded to nearest, as the oracle's expf (glibc, < 0.502 ulp) gives it: for |x| < 2^-7
+// (every sample of a 1024^3 volume at Fa <= 25) the Taylor form 1 + c, c = fma(x^2, q, -x),
+// q = 1/2 - x/6 + x^2/24, in fp32 -- -x is exact inside the fma, so c carries one rounding of a
+// term ~x^2/2 and the sum 1 + c rounds once at the granularity of the result; measured against
+// glibc's expf over 2.9e8 inputs in (-2^-7, 2^-7): 0.005 % differ (by one ulp), where the device
+// library's expf and the hardware exp2 differ far more often and with a bias.  That bias matters:
+// alpha = 1 - exp(-x) cancels, so one ulp of the exponential is ~2e-4 of a sample's opacity at this
+// step size, and a one-sided rounding adds up along every ray (C4's structure channel: 0.03 % of
+// the pixel value, rms 0.9 of the fp32 envelope).  Other x: exp in double, rounded.
+// Five fast VALU and no transcendental, against the mul, exp2 and sub of __expf.
+// the rare general case out of line (one copy per object instead of one per kernel variant)
+__device__ __attribute__((noinline)) float exp_neg_rn_general(float x) { return (float)exp(-(double)x); }
+__device__ __forceinline__ float exp_neg_rn(float x) {
+  const float x2 = x * x;
+  const float q = fmaf(x, fmaf(x, 1.f / 24.f, -1.f / 6.f), 0.5f);
+  float e = 1.f + fmaf(x2, q, -x);
+  if (__builtin_expect(!__all(fabsf(x) < 0x1p-7f), 0))  // wave-uniform: large or non-finite x
+    if (!(fabsf(x) < 0x1p-7f)) e = exp_neg_rn_general(x);
+  return e;
+}
+
+// 1 - __expf(-a * dx) (volumeRender_kernel.cu:456), both shading variants: the oracle's expf
+// (exp_neg_rn) -- x = a * dx rounded, then the exponential of its negation, as the oracle's
+// expf((-a) * dx) (negation is exact).
 template <bool FAST>
 __device__ __forceinline__ float opacity(float a, float tstep) {
 #if VR_ABLATE & 8
   return a * tstep;
 #else
-  if constexpr (FAST) return 1.f - __builtin_amdgcn_exp2f((-a * tstep) * 0x1.715476p+0f);
-  else return 1.f - expf(-a * tstep);
+  return 1.f - exp_neg_rn(a * tstep);
 #endif
 }
 
