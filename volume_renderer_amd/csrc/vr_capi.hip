@@ -663,6 +663,19 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
     if (const char *ev = std::getenv("VR_NO_EMPTY_SKIP"))  // A/B switch for measurements
       if (ev[0] == '1') P.skip_empty = 0;
   }
+  // Per-sample range tests the upload statistics decide for the whole launch (vr_sampling.h): every
+  // opacity argument |Fa * ab(p) * tstep| below 2^-7 (the exponential's Taylor form needs no
+  // per-sample check), and every |Fe * em(p) * tstep| finite (the empty-sample skip needs no
+  // per-sample magnitude test).  A trilinear sample never exceeds its texture's largest |voxel|.
+  {
+    const BufPtr &eb = g_tex.bind[g_tex.idx_em], &ab = g_tex.bind[g_tex.idx_ab];
+    auto vmax = [](const BufPtr &b) { return (b && b->ptr) ? (b->nonfinite ? INFINITY : (double)b->maxabs) : 0.0; };
+    const double xa = std::fabs((double)P.fa) * vmax(ab) * (double)P.tstep;
+    const double xe = std::fabs((double)P.fe) * vmax(eb) * (double)P.tstep;
+    P.small_x = (std::isfinite(xa) && xa < 0x1p-7 * 0.999) ? 1 : 0;
+    P.eds_finite = (std::isfinite(xe) && xe < 1e38) ? 1 : 0;
+    if (env_flag("VR_NO_RANGE_FLAGS")) P.small_x = P.eds_finite = 0;  // A/B and test switch
+  }
   F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
           is_big(P.gz) || env_flag("VR_FORCE_BIG");  // test switch: the 64-bit path on small volumes
   if (is_big(P.lut)) return fail(VR_ERR_UNSUPPORTED, "illumination volume larger than 2^32 voxels");

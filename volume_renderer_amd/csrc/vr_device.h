@@ -59,6 +59,8 @@ struct RenderParams {
   const float *gvec;              // lookup gradient interleaved (gx,gy,gz,0) x padded voxels, or null
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
+  int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test
+  int32_t eds_finite;             // every |Fe * em(p) * tstep| finite: empty skip without its test
   float tau;                      // host only: texels a pixel spans at the volume (depth_lanes)
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)
   int32_t xcd_run;                // march, unscheduled: runs of this many consecutive blocks per XCD (0/1: off)

@@ -21,6 +21,9 @@
 #ifndef VR_MARCH_K
 #define VR_MARCH_K 1  // depth lanes of this object file (see below)
 #endif
+#ifndef VR_MERGED_BOUNDS
+#define VR_MERGED_BOUNDS 1  // one wave-uniform slot test for the centre and the half-texel taps
+#endif
 #ifndef VR_BRANCHFREE_LEAP
 #define VR_BRANCHFREE_LEAP 1  // empty-chunk leap of K = 1 lanes without per-step branches
 #endif
@@ -162,28 +165,41 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   const int ac = ayz + lx;
   Cell C;  // the centre's partial sums, for the half-texel taps (valid where the centre is staged)
   float em_s;
+  // The half-texel taps of every lane in the slot (cells a - 1 .. a + 1 per axis, a = i + hi): then
+  // the centre cell is too (a - 1 >= 0 and a + 1 <= e - 2 put i in [0, e - 2]), so one wave-uniform
+  // test serves the centre fetch and the gradient, with no per-lane branch on either
+  bool full = false;
+  if constexpr (HALF_ONLY && VR_MERGED_BOUNDS)
+    full = __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
+                 (unsigned)(ly + (sy.hi ? 1 : 0) - 1) < (unsigned)(B.ey - 2) &&
+                 (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2));
   if constexpr (HALF_TAPS) {
-    if (staged && inx && iny && inz) em_s = lds_tri_cell(L, B, ac, ax.w, ay.w, az.w, C);
-    else em_s = fetch<BIG>(E, clamp_ax(ax, E.nx), clamp_ax(ay, E.ny), clamp_ax(az, E.nz));
+    if (full) em_s = lds_tri_cell(L, B, ac, ax.w, ay.w, az.w, C);
+    else if (staged && inx && iny && inz) em_s = lds_tri_cell(L, B, ac, ax.w, ay.w, az.w, C);
+    else {
+      const DevTex U = reload(E);
+      em_s = fetch<BIG>(U, clamp_ax(ax, U.nx), clamp_ax(ay, U.ny), clamp_ax(az, U.nz));
+    }
   } else {
     em_s = fetch_at<BIG>(E, L, B, staged && inx && iny && inz, ac, ax, ay, az);
   }
   const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
   const float e = P.fe * em_s;
   const float a = P.fa * ab_s;
-  alpha = opacity<VR_MARCH_FAST>(a, tstep);
+  const bool small_x = P.small_x != 0;  // wave-uniform: no per-sample range tests (vr_capi.hip)
+  alpha = small_x ? opacity<VR_MARCH_FAST>(a, tstep, true) : opacity<VR_MARCH_FAST>(a, tstep);
   const float eds = e * tstep;
   float ir = 0.f, ig = 0.f, ib = 0.f;
-  const bool skip = P.skip_empty && alpha == 0.f && fabsf(eds) <= 3.0e38f;
+  const bool skip = P.skip_empty && alpha == 0.f && (P.eds_finite || fabsf(eds) <= 3.0e38f);
   shaded = MODE != 0 && !skip;
   if (MODE != 0 && !skip) {
     f3 g;
     if (MODE == 1 && (VR_ABLATE & 4)) {
       g = mk(ps.x, ps.y, em_s);
     } else if (HALF_TAPS && (HALF_ONLY || P.tap_half) &&
-               __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
+               (full || __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
                      (unsigned)(ly + (sy.hi ? 1 : 0) - 1) < (unsigned)(B.ey - 2) &&
-                     (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2))) {
+                     (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2)))) {
       // every shading lane's taps lie in the staged box (the tap cells a - 1 .. a + 1 per axis,
       // a = i + hi): the taps from the slot with their shared voxels and partial sums
       // unhalved: the fast shading uses g only through n = -g * rsq(g.g), which the exact factor 2
@@ -601,6 +617,11 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   }
 }
 
+#if VR_ISA_PROBE
+// ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation, for a quick look
+// at its code (VGPR / SGPR use, spills, the sample loop) without compiling every variant.
+template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);
+#else
 #if VR_MARCH_K <= 4
 // One wave's tile of workgroup `wg` of a view: ray setup, the march, the pixel store into `out` --
 // march_kernel's body for the multi-view launch below.  (march_kernel keeps its own copy: routed
@@ -918,5 +939,6 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
   }
 }
 
+#endif  // VR_ISA_PROBE
 }  // namespace fast / exact
 }  // namespace vr

@@ -410,7 +410,10 @@ __device__ __forceinline__ float acospi_q(float q) {
   p = fmaf(p, t, -6.830968708e-02f);
   p = fmaf(p, t, 0.5f);
   const float r = __builtin_amdgcn_sqrtf(1.f - t) * p;
-  return q < 0.f ? 1.f - r : r;
+  // q < 0 ? 1 - r : r without a compare: fma(-1, r, 1) rounds as 1 - r, fma(1, r, 0) is r (q = -0
+  // takes the first form: 1 - 0.5 = 0.5 = r, the same value)
+  const float sg = __builtin_copysignf(1.f, q);
+  return fmaf(sg, r, fmaf(-0.5f, sg, 0.5f));
 #else
   return __ocml_acospi_f32(q);
 #endif
@@ -428,11 +431,12 @@ __device__ __forceinline__ float acospi_q(float q) {
 // Five fast VALU and no transcendental, against the mul, exp2 and sub of __expf.
 // the rare general case out of line (one copy per object instead of one per kernel variant)
 __device__ __attribute__((noinline)) float exp_neg_rn_general(float x) { return (float)exp(-(double)x); }
-__device__ __forceinline__ float exp_neg_rn(float x) {
+// small: the host proved |x| < 2^-7 for every sample of the launch (RenderParams::small_x).
+__device__ __forceinline__ float exp_neg_rn(float x, bool small = false) {
   const float x2 = x * x;
   const float q = fmaf(x, fmaf(x, 1.f / 24.f, -1.f / 6.f), 0.5f);
   float e = 1.f + fmaf(x2, q, -x);
-  if (__builtin_expect(!__all(fabsf(x) < 0x1p-7f), 0))  // wave-uniform: large or non-finite x
+  if (!small && __builtin_expect(!__all(fabsf(x) < 0x1p-7f), 0))  // wave-uniform: large or non-finite x
     if (!(fabsf(x) < 0x1p-7f)) e = exp_neg_rn_general(x);
   return e;
 }
@@ -441,11 +445,11 @@ __device__ __forceinline__ float exp_neg_rn(float x) {
 // (exp_neg_rn) -- x = a * dx rounded, then the exponential of its negation, as the oracle's
 // expf((-a) * dx) (negation is exact).
 template <bool FAST>
-__device__ __forceinline__ float opacity(float a, float tstep) {
+__device__ __forceinline__ float opacity(float a, float tstep, bool small = false) {
 #if VR_ABLATE & 8
   return a * tstep;
 #else
-  return 1.f - exp_neg_rn(a * tstep);
+  return 1.f - exp_neg_rn(a * tstep, small);
 #endif
 }
 

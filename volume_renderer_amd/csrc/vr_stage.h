@@ -53,6 +53,10 @@ __device__ __forceinline__ int wave_reduce(int v) {
 __device__ __forceinline__ int wave_min(int v) { return wave_reduce<false>(v); }
 __device__ __forceinline__ int wave_max(int v) { return wave_reduce<true>(v); }
 
+#ifndef VR_RELOAD_TEX
+#define VR_RELOAD_TEX 0
+#endif
+
 #ifndef VR_ODD_PITCH
 // LDS row / plane pitches: 0 dense (ex, ex * ey); 1 always odd (measured slower: the larger slots
 // overflow more); 2 odd when the padded box still fits the slot, dense otherwise
@@ -145,6 +149,32 @@ __device__ __forceinline__ bool in_box(int l, int e) {
   return (VR_ABLATE & 16) || (unsigned)l < (unsigned)(e - 1);
 }
 
+// A texture's parameters re-read from the kernel-argument segment at the point of use (scalar loads)
+// for the rare global-memory taps: behind the empty asm the compiler cannot hoist the loads out of
+// the sample loop, so they do not hold SGPRs across it (the loop's SGPRs spill to VGPR lanes
+// otherwise, and every spilled value costs a v_readlane per use).
+__device__ __forceinline__ DevTex reload(const DevTex &t) {
+#if VR_RELOAD_TEX == 1
+  typedef const volatile __attribute__((address_space(4))) DevTex *cptr;
+  cptr q = (cptr)&t;
+  DevTex u;
+  u.p = q->p;
+  u.nx = q->nx;
+  u.ny = q->ny;
+  u.nz = q->nz;
+  u.px = q->px;
+  u.pxy = q->pxy;
+  return u;
+#elif VR_RELOAD_TEX == 2
+  typedef const __attribute__((address_space(4))) DevTex *cptr;
+  cptr q = (cptr)&t;
+  asm volatile("" : "+s"(q));
+  return *q;
+#else
+  return t;
+#endif
+}
+
 // Trilinear fetch of the staged emission texture: the slot when the 2x2x2 cell lies in the box
 // (`in`, with slot word `a`), global memory otherwise -- the same interpolation either way.  The
 // axes are unclamped (axis_raw); the global path clamps them.
@@ -152,7 +182,8 @@ template <bool BIG>
 __device__ __forceinline__ float fetch_at(const DevTex &t, const float *L, const Box &B, bool in, int a,
                                           const Ax &ax, const Ax &ay, const Ax &az) {
   if (in) return lds_tri(L, B, a, ax.w, ay.w, az.w);
-  return fetch<BIG>(t, clamp_ax(ax, t.nx), clamp_ax(ay, t.ny), clamp_ax(az, t.nz));
+  const DevTex u = reload(t);
+  return fetch<BIG>(u, clamp_ax(ax, u.nx), clamp_ax(ay, u.ny), clamp_ax(az, u.nz));
 }
 
 // Padded index range [lo, hi] (inclusive) of the tap pairs of one axis for a coordinate range.
