@@ -909,6 +909,9 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
         return hipSuccess;  // no schedule
       }
     }
+    // VR_SCHED_ROWS=1 (A/B): tile rows of workgroups in the order of their heaviest block, each row
+    // in its own order -- the heavy band early, row-major neighbours still together
+    const bool rows = env_flag("VR_SCHED_ROWS");
     if (S.copy_pending && hipEventQuery(S.copied) == hipSuccess) {  // the last measurement arrived
       S.copy_pending = false;
       uint64_t sum = 0;
@@ -918,9 +921,27 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
         mx = std::max(mx, S.h_cost[i]);
       }
       const uint64_t wg_slots = std::max<uint64_t>(1, (uint64_t)(device_wave_slots() / 16 * 6));
-      S.tail = (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
+      S.tail = rows || (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
       S.decided = true;
       S.order_stale = true;
+      if (rows) {  // workgroup wg is tile block (wg % nbx, wg / nbx) (vr_march.hip march_kernel)
+        const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
+        const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
+        const uint32_t nr = (nb + nbx - 1) / nbx;
+        std::vector<std::pair<uint32_t, uint32_t>> rk(nr);
+        for (uint32_t r = 0; r < nr; ++r) {
+          uint32_t m = 0;
+          for (uint32_t i = r * nbx; i < std::min(nb, (r + 1) * nbx); ++i) m = std::max(m, S.h_cost[i]);
+          rk[r] = {m, r};
+        }
+        std::stable_sort(rk.begin(), rk.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+        std::vector<uint32_t> ord;
+        ord.reserve(nb);
+        for (const auto &x : rk)
+          for (uint32_t i = x.second * nbx; i < std::min(nb, (x.second + 1) * nbx); ++i) ord.push_back(i);
+        VR_HIP(hipMemcpy(S.d_order, ord.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice));
+        S.order_stale = false;
+      }
     }
     (void)hipGetLastError();
     bool measure = !S.measured;

@@ -617,11 +617,6 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   }
 }
 
-#if VR_ISA_PROBE
-// ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation, for a quick look
-// at its code (VGPR / SGPR use, spills, the sample loop) without compiling every variant.
-template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);
-#else
 #if VR_MARCH_K <= 4
 // One wave's tile of workgroup `wg` of a view: ray setup, the march, the pixel store into `out` --
 // march_kernel's body for the multi-view launch below.  (march_kernel keeps its own copy: routed
@@ -688,6 +683,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, false)) void ma
                                                           P.out, R, C);
 }
 
+#if !VR_ISA_PROBE
 // Host entry (launch_march_views_k1 / _k2 / _k4): V.p[0 .. nviews) share the image, partition,
 // gradient mode (0 or 1), absorption aliasing and slot size; 32-bit addressing only.
 hipError_t VR_CAT(launch_march_views_k, VR_MARCH_K)(const RenderViews &V, uint32_t nviews, int mode, bool ab_alias,
@@ -724,6 +720,7 @@ hipError_t VR_CAT(launch_march_views_k, VR_MARCH_K)(const RenderViews &V, uint32
   return hipGetLastError();
 }
 
+#endif  // !VR_ISA_PROBE
 // Sort-last slab launch: one wave per 8x8 tile of the image part (the columns of
 // the image partition, vr_partition); per pixel the ray state is read from P.slab_in (null: a
 // fresh ray), marched through this slab's samples and written to P.out as VR_SLAB_PLANES
@@ -818,6 +815,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= 1664 && !SCHED) ? VR_SLAB
   }
 }
 
+#if !VR_ISA_PROBE
 // Host entry of the slab launch (launch_march_slab_k1 / _k2 / _k4): MODE 0 or 1, absorption
 // aliasing emission, the emission texture addressed with 64-bit offsets from its virtual base.
 template <int MODE, bool SH, int CAP>
@@ -848,8 +846,10 @@ hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mo
   else launch_slab_m<1, false>(P, grid, s);
   return hipGetLastError();
 }
+#endif  // !VR_ISA_PROBE
 #endif
 
+#if !VR_ISA_PROBE
 // Diagnostics (VR_LDS_PAD=bytes): unused dynamic LDS per workgroup of a short scheduled launch,
 // to cap the workgroups a CU holds (the heavy waves' co-residency).
 static unsigned short_launch_lds_pad() {
@@ -939,6 +939,11 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
   }
 }
 
-#endif  // VR_ISA_PROBE
+#else
+// ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation and the matching
+// sort-last slab kernel, for a quick look at their code without compiling every variant.
+template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);
+template __global__ void march_slab_kernel<2, 1, true, VR_LDS_CAP, false>(const RenderParams P);
+#endif  // !VR_ISA_PROBE
 }  // namespace fast / exact
 }  // namespace vr

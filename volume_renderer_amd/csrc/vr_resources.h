@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -361,8 +363,21 @@ struct Uploader {
   }
 
   // src (host or device, per `on_device`) -> dst (padded, (nx+2)(ny+2)(nz+2) floats); *st = stats
+  static bool timing() {
+    static const bool on = [] {
+      const char *ev = std::getenv("VR_UPLOAD_TIMING");
+      return ev && ev[0] == '1';
+    }();
+    return on;
+  }
+  static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+
   hipError_t upload(const float *src, bool on_device, int32_t nx, int32_t ny, int32_t nz, float *dst,
                     vr::BufStats *st) {
+    const double t0 = now_ms();
+    double t_copied = t0;
     hipError_t rc = hipMemsetAsync(d_stats, 0, sizeof(vr::BufStats), pad_stream);
     const uint64_t plane = (uint64_t)nx * (uint64_t)ny;
     if (rc == hipSuccess && on_device) {
@@ -400,8 +415,19 @@ struct Uploader {
       }
     }
     if (rc == hipSuccess) rc = hipMemcpyAsync(h_stats, d_stats, sizeof(vr::BufStats), hipMemcpyDeviceToHost, pad_stream);
+    if (rc == hipSuccess && timing()) {  // diagnostics: when the copies and the pads ended
+      hipEvent_t ce = nullptr;
+      if (hipEventCreate(&ce) == hipSuccess && hipEventRecord(ce, stream) == hipSuccess) {
+        (void)hipEventSynchronize(ce);
+        t_copied = now_ms();
+      }
+      if (ce) (void)hipEventDestroy(ce);
+    }
     if (rc == hipSuccess) rc = hipStreamSynchronize(pad_stream);  // the last pad followed the last copy
     if (rc == hipSuccess) rc = hipStreamSynchronize(stream);
+    if (rc == hipSuccess && timing())
+      std::fprintf(stderr, "VR_UPLOAD_TIMING bytes %llu copies %.2f ms total %.2f ms\n",
+                   (unsigned long long)(plane * (uint64_t)nz * sizeof(float)), t_copied - t0, now_ms() - t0);
     if (rc == hipSuccess) *st = *h_stats;
     return rc;
   }
