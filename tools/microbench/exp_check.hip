@@ -12,7 +12,7 @@
 
 __device__ __forceinline__ float exp_neg_rn_dev(float x) {
   const float x2 = x * x;
-  const float q = fmaf(x, fmaf(x, 1.f / 24.f, -1.f / 6.f), 0.5f);
+  const float q = fmaf(x, x * (1.f / 24.f) + (-1.f / 6.f), 0.5f);
   return 1.f + fmaf(x2, q, -x);
 }
 

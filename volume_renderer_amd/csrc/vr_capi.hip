@@ -676,6 +676,12 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
     P.eds_finite = (std::isfinite(xe) && xe < 1e38) ? 1 : 0;
     if (env_flag("VR_NO_RANGE_FLAGS")) P.small_x = P.eds_finite = 0;  // A/B and test switch
   }
+  {
+    const bool re_ok = P.re_is_em || (P.re.p && P.re.one);
+    const bool lut_ok = g_tex.lights.empty() || (P.lut.p && P.lut.small && !P.lut.one);
+    P.tame = (P.skip_empty && P.eds_finite && P.small_x && re_ok && lut_ok && !env_flag("VR_NO_TAME")) ? 1 : 0;
+    P.re_mask = P.re_is_em ? 0xffffffffu : 0u;
+  }
   F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
           is_big(P.gz) || env_flag("VR_FORCE_BIG");  // test switch: the 64-bit path on small volumes
   if (is_big(P.lut)) return fail(VR_ERR_UNSUPPORTED, "illumination volume larger than 2^32 voxels");

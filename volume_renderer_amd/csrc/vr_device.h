@@ -61,6 +61,11 @@ struct RenderParams {
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test
   int32_t eds_finite;             // every |Fe * em(p) * tstep| finite: empty skip without its test
+  // "tame" launch (the march's fast path, vr_march.hip): skip_empty, eds_finite and small_x hold,
+  // the reflection texture is the emission texture or a single voxel, and the LUT (if lights) is a
+  // bound grid below 2^22 padded voxels -- every launch-wide test of the sample loop decided here
+  int32_t tame;
+  uint32_t re_mask;               // tame: ~0 if the reflection sample is the emission sample, else 0
   float tau;                      // host only: texels a pixel spans at the volume (depth_lanes)
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)
   int32_t xcd_run;                // march, unscheduled: runs of this many consecutive blocks per XCD (0/1: off)

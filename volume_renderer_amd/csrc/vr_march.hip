@@ -186,11 +186,16 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   const float ab_s = AB_ALIAS ? em_s : tex3d<BIG>(P.ab, ps.x, ps.y, ps.z);
   const float e = P.fe * em_s;
   const float a = P.fa * ab_s;
-  const bool small_x = P.small_x != 0;  // wave-uniform: no per-sample range tests (vr_capi.hip)
-  alpha = small_x ? opacity<VR_MARCH_FAST>(a, tstep, true) : opacity<VR_MARCH_FAST>(a, tstep);
+  // NANCHK = false is the tame fast path (march_kernel: finite rays of a launch with P.tame): every
+  // launch-wide test below was decided by the host (vr_capi.hip), so none of them holds a uniform
+  // mask in SGPRs across the sample loop (such masks spill to VGPR lanes and cost a v_readlane pair
+  // per use)
+  constexpr bool TAME = !NANCHK;
+  if constexpr (TAME) alpha = opacity<VR_MARCH_FAST>(a, tstep, true);
+  else alpha = P.small_x ? opacity<VR_MARCH_FAST>(a, tstep, true) : opacity<VR_MARCH_FAST>(a, tstep);
   const float eds = e * tstep;
   float ir = 0.f, ig = 0.f, ib = 0.f;
-  const bool skip = P.skip_empty && alpha == 0.f && (P.eds_finite || fabsf(eds) <= 3.0e38f);
+  const bool skip = TAME ? alpha == 0.f : (P.skip_empty && alpha == 0.f && (P.eds_finite || fabsf(eds) <= 3.0e38f));
   shaded = MODE != 0 && !skip;
   if (MODE != 0 && !skip) {
     f3 g;
@@ -260,8 +265,15 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
       g = mk(tex3d<BIG>(P.gx, ps.x, ps.y, ps.z), tex3d<BIG>(P.gy, ps.x, ps.y, ps.z),
              tex3d<BIG>(P.gz, ps.x, ps.y, ps.z));
     }
-    const float refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
-    shade_lights<VR_MARCH_FAST>(P, g, pos, o, refl, ir, ig, ib);
+    float refl;
+    if constexpr (TAME) {  // the emission sample or the single voxel, selected by a 32-bit mask (v_bfi)
+      const float v = P.re.p[0];
+      const uint32_t m = P.re_mask;
+      refl = P.fr * __uint_as_float((__float_as_uint(em_s) & m) | (__float_as_uint(fmaf(0.5f, v - v, v)) & ~m));
+    } else {
+      refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
+    }
+    shade_lights<VR_MARCH_FAST, TAME>(P, g, pos, o, refl, ir, ig, ib);
   }
   r = fmaf(eds, P.color[0], ir) * alpha;
   gg = fmaf(eds, P.color[1], ig) * alpha;
@@ -578,8 +590,9 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
     R.t = tnear;
   }
-  // every coordinate the march forms from a finite start and step is finite
-  if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+  // every coordinate the march forms from a finite start and step is finite; a tame launch takes
+  // the fast path (sample_at: TAME)
+  if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
   else
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
@@ -650,8 +663,9 @@ __device__ __forceinline__ void march_tile(const RenderParams &P, float *L, int 
     R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
     R.t = tnear;
   }
-  // every coordinate the march forms from a finite start and step is finite
-  if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+  // every coordinate the march forms from a finite start and step is finite; a tame launch takes
+  // the fast path (sample_at: TAME)
+  if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
   else
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
@@ -795,7 +809,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= 1664 && !SCHED) ? VR_SLAB
   }
   // the resume point as it stands (a ray passed through keeps it; one handed off below replaces it)
   if (active && (lane & (K - 1)) == 0) store_resume(P, kk, R.t, R.pos, R.nsteps);
-  if (__all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+  if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
     march<K, MODE, true, false, SH, true, false, CAP, true>(P, L, lane, R, C, kk);
   else
     march<K, MODE, true, false, SH, true, true, CAP, true>(P, L, lane, R, C, kk);

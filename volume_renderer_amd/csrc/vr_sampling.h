@@ -390,6 +390,9 @@ __device__ __forceinline__ float divpi(float x) {
 #ifndef VR_FAST_ACOS
 #define VR_FAST_ACOS 1
 #endif
+#ifndef VR_ACOS_LITERALS
+#define VR_ACOS_LITERALS 1
+#endif
 #ifndef VR_FAST_NLEN
 #define VR_FAST_NLEN 1  // 1: the fast variant takes the unit normal's length as 1 (shade_lights)
 #endif
@@ -400,6 +403,24 @@ extern "C" __device__ float __ocml_acospi_f32(float);
 __device__ __forceinline__ float acospi_q(float q) {
 #if VR_FAST_ACOS
   const float t = fabsf(q);
+#if VR_ACOS_LITERALS
+  // the Horner steps as VOP2 v_fmaak_f32 with the coefficient as a literal: written as plain fmaf the
+  // compiler folds |q| into VOP3 fmas, which take no literal on gfx950, and holds the eight
+  // coefficients in SGPRs across the sample loop -- where they push other values into v_readlane
+  // spills.  Same single rounding per step (d = s0 * s1 + K).
+  float p;
+  asm("v_mov_b32 %0, 0x3967ab32\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0xbaa77072\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0x3b67639e\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0xbbd8c4b8\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0x3c2a004e\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0xbc83f1fe\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0x3ce82823\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0xbd8be5f3\n\t"
+      "v_fmaak_f32 %0, %0, %1, 0x3f000000"
+      : "=&v"(p)
+      : "v"(t));
+#else
   float p = 2.209365193e-04f;
   p = fmaf(p, t, -1.277460018e-03f);
   p = fmaf(p, t, 3.530717921e-03f);
@@ -409,6 +430,7 @@ __device__ __forceinline__ float acospi_q(float q) {
   p = fmaf(p, t, 2.833945118e-02f);
   p = fmaf(p, t, -6.830968708e-02f);
   p = fmaf(p, t, 0.5f);
+#endif
   const float r = __builtin_amdgcn_sqrtf(1.f - t) * p;
   // q < 0 ? 1 - r : r without a compare: fma(-1, r, 1) rounds as 1 - r, fma(1, r, 0) is r (q = -0
   // takes the first form: 1 - 0.5 = 0.5 = r, the same value)
@@ -434,7 +456,10 @@ __device__ __attribute__((noinline)) float exp_neg_rn_general(float x) { return 
 // small: the host proved |x| < 2^-7 for every sample of the launch (RenderParams::small_x).
 __device__ __forceinline__ float exp_neg_rn(float x, bool small = false) {
   const float x2 = x * x;
-  const float q = fmaf(x, fmaf(x, 1.f / 24.f, -1.f / 6.f), 0.5f);
+  // q = 1/2 - x/6 + x^2/24: its own rounding enters c only through x^2 q (relative 2^-23 of a term
+  // below 2^-15), so the inner term is a mul and an add with literal operands (VOP2) -- an fma would
+  // need one of its constants held in a register across the sample loop
+  const float q = fmaf(x, x * (1.f / 24.f) + (-1.f / 6.f), 0.5f);
   float e = 1.f + fmaf(x2, q, -x);
   if (!small && __builtin_expect(!__all(fabsf(x) < 0x1p-7f), 0))  // wave-uniform: large or non-finite x
     if (!(fabsf(x) < 0x1p-7f)) e = exp_neg_rn_general(x);
@@ -458,7 +483,9 @@ __device__ __forceinline__ float opacity(float a, float tstep, bool small = fals
 // dot(a,b) * rsq(a.a) * rsq(b.b) with the hardware reciprocal square root (1 ulp, as the
 // reference's own rsqrtf normalize) and acos/pi in one step; within the parity tolerance of
 // SURVEY.md 8c, about 10 % faster at the metric configuration.
-template <bool FAST>
+// TAME (vr_march.hip sample_at): the launch's LUT, if it has lights, is a bound grid of fewer than
+// 2^22 padded voxels (RenderParams::tame), so only the fetch_small path is compiled.
+template <bool FAST, bool TAME = false>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib) {
 #if !VR_FAST_COS
@@ -516,7 +543,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     const float alpha_n = acospi_q(dot3(n, li) * (rn * __builtin_amdgcn_rsqf(dot3(li, li))));
     const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
     int i = 0;
-    if (P.lut.p != nullptr && P.lut.small && !P.lut.one) {
+    if (TAME || (P.lut.p != nullptr && P.lut.small && !P.lut.one)) {
       // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
       // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
       for (; i + 1 < P.num_lights; i += 2) {
@@ -543,7 +570,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
         ib = fmaf(rl1 * L1.cb, P.color[2], ib);
       }
     }
-    for (; i + 1 < P.num_lights; i += 2) {
+    if constexpr (!TAME) for (; i + 1 < P.num_lights; i += 2) {
       const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
       const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
       const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
@@ -572,7 +599,9 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
       const float beta = acospi_q(dlo * (rn * __builtin_amdgcn_rsqf(dot3(lo, lo))));
       const float gamma = acospi_q(dot3(lip, lop) * (rlip * __builtin_amdgcn_rsqf(dot3(lop, lop))));
-      const float rl = refl * lut_light<true>(P.lut, la, beta, gamma);
+      const float rl = refl * (TAME ? fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
+                                                  axis_lut<true>(gamma, P.lut.fnz))
+                                    : lut_light<true>(P.lut, la, beta, gamma));
       ir = fmaf(rl * L.cr, P.color[0], ir);
       ig = fmaf(rl * L.cg, P.color[1], ig);
       ib = fmaf(rl * L.cb, P.color[2], ib);
