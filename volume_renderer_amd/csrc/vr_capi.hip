@@ -138,9 +138,22 @@ struct HipError {
 
 #define VR_HIP(call)                                 \
   do {                                               \
+    trace_pending(#call);                            \
     hipError_t e_ = (call);                          \
     if (e_ != hipSuccess) throw HipError{e_, #call}; \
   } while (0)
+
+// VR_TRACE_STALE=1 (diagnostics): name the checked call before which this thread's HIP error state
+// already held an error (one a later hipGetLastError-based check would otherwise report)
+inline void trace_pending(const char *what) {
+  static const bool on = [] {
+    const char *ev = std::getenv("VR_TRACE_STALE");
+    return ev && ev[0] == '1';
+  }();
+  if (!on) return;
+  const hipError_t e = hipPeekAtLastError();
+  if (e != hipSuccess) std::fprintf(stderr, "VR_TRACE_STALE before %s: %s\n", what, hipGetErrorString(e));
+}
 
 // texture ids = the reference's vr::VolumeType (volumeRender.h:149-157)
 enum TexId { T_EM = 0, T_AB = 1, T_RE = 2, T_DX = 3, T_DY = 4, T_DZ = 5, T_LIGHT = 6, T_COUNT = 7 };
@@ -1399,7 +1412,17 @@ void delete_children(vr_context *h) {
   h->children.clear();
 }
 
-#define VR_GUARD_BEGIN try {
+// An error left in this thread's HIP error state by an earlier caller (another library, a call of
+// ours whose error was handled) must not be reported by this call's checks: cleared at entry
+// (VR_TRACE_STALE=1 prints it).
+inline void clear_stale(const char *fn) {
+  const hipError_t e = hipGetLastError();
+  static const bool trace = env_flag("VR_TRACE_STALE");
+  if (e != hipSuccess && trace) std::fprintf(stderr, "VR_TRACE_STALE %s: %s\n", fn, hipGetErrorString(e));
+}
+#define VR_GUARD_BEGIN \
+  clear_stale(__func__); \
+  try {
 #define VR_GUARD_END                                                                             \
   }                                                                                              \
   catch (const HipError &e) {                                                                    \
