@@ -21,6 +21,7 @@ Configs (BASELINE.json "configs"):
 C1 (64^3, 256x256, EA only) is checked whole in test_gpu_parity.py / test_gpu_golden.py.
 """
 import json
+import os
 
 import numpy as np
 import pytest
@@ -38,6 +39,10 @@ THREADS = 16  # the GPU box's CPU share (os.cpu_count() there reports the whole 
 # the product may be at most half as far from the fp32 oracle (RMS over lit sampled channels) as the
 # fp32 oracle is from exact arithmetic (fp64), at every full-size config, default shading included
 MAX_RMS_RATIO = 0.5
+# and the unfloored SURVEY.md 8c fraction itself: the exact-op kernel meets the SURVEY's 99.9 %, the
+# default (fast) arithmetic at least 99.8 % at every config (measured 99.90-100 %)
+MIN_SURVEY_EXACT = 0.999
+MIN_SURVEY_FAST = 0.998
 EX1_LIGHTS = np.array([[500, 1000, 550, 0, 1, 1], [0, 550, 90, 1, 0.5, 1]], np.float32)
 EX3_LIGHT = np.array([[-15, 15, 0, 0.5, 0.5, 0.5]], np.float32)
 
@@ -150,6 +155,8 @@ def oracle_check(S, h, lights, lut, rargs, img, R, props, bmax, what, seed=1):
                  uniform_rms_ratio=u["rms_ratio"])
     print("PARITY", json.dumps(dict(what=what, **stats)))
     assert stats["samples"] > 100 * len(xs) and ref32.max() > 0
+    min_survey = MIN_SURVEY_EXACT if os.environ.get("VR_EXACT_SHADE") == "1" else MIN_SURVEY_FAST
+    assert stats["frac_within_survey"] >= min_survey, (what, stats)
     return stats
 
 
@@ -225,8 +232,9 @@ def test_c2_1024x768_compute_gradient(monkeypatch):
                                  (1, 1, 1), f"C2 V_shell(1024) 1024x768 {shade}")
         vr.volumeRender("delete", sc["h"])
         del sc
-    # only acosf comes from another library in the exact kernel: much closer than fp32 rounding
-    assert st["exact"]["rms_ratio"] <= 0.25, st["exact"]
+    # only acosf comes from another library in the exact kernel: ~1000x closer than fp32 rounding
+    # (measured rms ratio 0.0008)
+    assert st["exact"]["rms_ratio"] <= 0.01, st["exact"]
     assert st["fast"]["frac_within_survey"] >= st["exact"]["frac_within_survey"] - 0.005, st
 
 
