@@ -772,3 +772,23 @@ def test_full_frame_schedule_keeps_the_image(monkeypatch, counter_clock, tail_pc
     for k, (a, b) in enumerate(zip(frames["sched"], frames["plain"])):
         assert a.max() > 0
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+
+
+def test_bounce_upload_is_bit_identical(monkeypatch, counter_clock):
+    """A host volume uploaded through the pinned bounce ring (VR_UPLOAD_BOUNCE=1, vr_resources.h
+    Bounce: 16 MiB pieces through 16 pinned buffers filled by 3 host threads) renders bit for bit as
+    the runtime's pageable copy.  322 MB of ragged extent: 20 pieces (the ring wraps), the last one
+    partial."""
+    rng = np.random.default_rng(5)
+    data = np.asfortranarray(rng.random((430, 433, 431), dtype=np.float32) * np.float32(0.02))
+    v = vr.Volume(data)
+    r = ex1_renderer(v, res=(96, 80))
+    monkeypatch.setenv("VR_UPLOAD_BOUNCE", "0")
+    base = r.render()
+    monkeypatch.setenv("VR_UPLOAD_BOUNCE", "1")
+    monkeypatch.setenv("VR_UPLOAD_THREADS", "3")
+    v.touch()
+    got = r.render()
+    assert base.max() > 0
+    assert np.array_equal(got.view(np.uint32), base.view(np.uint32))
+    r.delete()

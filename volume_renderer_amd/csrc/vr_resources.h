@@ -18,12 +18,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "vr_device.h"
@@ -320,6 +322,82 @@ struct LaunchRec {
 // Device volumes are padded straight from the caller's buffer.  The call returns when the volume
 // is resident (the caller's pointer is borrowed for the call only, render.cpp:307-342) -- renders
 // already in flight on other streams keep running meanwhile.
+// Pinned bounce ring for pageable host sources (the copy half of the upload path, SURVEY.md 8f row
+// 3; VR_UPLOAD_BOUNCE).  A pageable hipMemcpyAsync is staged by the runtime through its own pinned
+// buffers, one thread filling them; here the source crosses in PIECE-sized pieces through a ring of
+// NB pinned buffers that a pool of host threads fills in parallel (worker w copies pieces w, w + T,
+// ...), while the calling thread issues each filled piece's DMA in order on the copy stream.  A
+// buffer is refilled only after the DMA of the piece it last held has completed (its event).
+struct Bounce {
+  static constexpr size_t PIECE = 16ull << 20;
+  static constexpr int NB = 16;
+  char *pinned = nullptr;
+  hipEvent_t ev[NB] = {};
+
+  hipError_t init() {
+    if (pinned) return hipSuccess;
+    hipError_t rc = hipHostMalloc(reinterpret_cast<void **>(&pinned), PIECE * NB, hipHostMallocDefault);
+    for (int i = 0; i < NB && rc == hipSuccess; ++i) rc = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    if (rc != hipSuccess) {  // all or nothing
+      (void)hipGetLastError();
+      for (hipEvent_t &e : ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+      if (pinned) (void)hipHostFree(pinned);
+      pinned = nullptr;
+    }
+    return rc;
+  }
+
+  static int threads() {
+    const char *ev = std::getenv("VR_UPLOAD_THREADS");
+    return std::max(1, std::min(ev ? std::atoi(ev) : 8, NB));
+  }
+
+  // dst (device) <- src (pageable host), `bytes`, ordered on `stream`.  Returns once every piece's
+  // DMA is issued (the last ones may still be running).
+  hipError_t copy(void *dst, const void *src, size_t bytes, hipStream_t stream) {
+    const size_t np = (bytes + PIECE - 1) / PIECE;
+    if (!np) return hipSuccess;
+    const int T = (int)std::min<size_t>((size_t)threads(), np);
+    std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[np]);
+    for (size_t i = 0; i < np; ++i) ready[i].store(0, std::memory_order_relaxed);
+    std::atomic<size_t> issued{0};
+    std::atomic<bool> stop{false};
+    auto fill = [&](int w) {
+      for (size_t i = (size_t)w; i < np; i += (size_t)T) {
+        const int b = (int)(i % NB);
+        if (i >= (size_t)NB)  // the piece that last held buffer b has been issued ...
+          while (issued.load(std::memory_order_acquire) <= i - NB)
+            if (stop.load(std::memory_order_relaxed)) return;
+            else std::this_thread::yield();
+        (void)hipEventSynchronize(ev[b]);  // ... and its DMA has completed
+        const size_t off = i * PIECE;
+        std::memcpy(pinned + (size_t)b * PIECE, static_cast<const char *>(src) + off, std::min(PIECE, bytes - off));
+        ready[i].store(1, std::memory_order_release);
+      }
+    };
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)T);
+    for (int w = 0; w < T; ++w) pool.emplace_back(fill, w);
+    hipError_t rc = hipSuccess;
+    for (size_t i = 0; i < np; ++i) {
+      while (!ready[i].load(std::memory_order_acquire)) std::this_thread::yield();
+      const int b = (int)(i % NB);
+      const size_t off = i * PIECE;
+      rc = hipMemcpyAsync(static_cast<char *>(dst) + off, pinned + (size_t)b * PIECE, std::min(PIECE, bytes - off),
+                          hipMemcpyHostToDevice, stream);
+      if (rc == hipSuccess) rc = hipEventRecord(ev[b], stream);
+      if (rc != hipSuccess) {
+        stop.store(true);
+        break;
+      }
+      issued.store(i + 1, std::memory_order_release);
+    }
+    for (std::thread &t : pool) t.join();
+    return rc;
+  }
+};
+
 struct Uploader {
   static constexpr size_t CHUNK = 1ull << 30, WHOLE = 8ull << 30;
   static constexpr int NS = 4;
@@ -330,6 +408,12 @@ struct Uploader {
   float *staging = nullptr;  // nslots slots of slot_floats
   size_t slot_floats = 0, nslots = 0;
   vr::BufStats *d_stats = nullptr, *h_stats = nullptr;
+  Bounce bounce;  // VR_UPLOAD_BOUNCE=1: host sources through the pinned ring
+
+  static bool use_bounce() {
+    const char *ev = std::getenv("VR_UPLOAD_BOUNCE");
+    return ev && ev[0] == '1';
+  }
 
   hipError_t init(int d) {
     if (stream) return hipSuccess;
@@ -403,8 +487,11 @@ struct Uploader {
         const int k = (int)(c % nslots);
         float *slot = staging + (size_t)k * slot_floats;
         if (c >= nslots) rc = hipStreamWaitEvent(stream, padded[k], 0);  // the slot's previous chunk is padded
-        if (rc == hipSuccess)
-          rc = hipMemcpyAsync(slot, src + z0 * plane, (z1 - z0) * plane * sizeof(float), hipMemcpyHostToDevice, stream);
+        if (rc == hipSuccess) {
+          const size_t nbytes = (z1 - z0) * plane * sizeof(float);
+          if (use_bounce() && bounce.init() == hipSuccess) rc = bounce.copy(slot, src + z0 * plane, nbytes, stream);
+          else rc = hipMemcpyAsync(slot, src + z0 * plane, nbytes, hipMemcpyHostToDevice, stream);
+        }
         if (rc == hipSuccess) rc = hipEventRecord(copied[k], stream);
         if (rc == hipSuccess) rc = hipStreamWaitEvent(pad_stream, copied[k], 0);
         // padded planes: source plane z sits at z + 1; the apron planes 0 and nz + 1 replicate the ends
