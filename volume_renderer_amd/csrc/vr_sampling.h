@@ -401,6 +401,9 @@ __device__ __forceinline__ float divpi(float x) {
 #endif
 extern "C" __device__ float __ocml_acospi_f32(float);
 __device__ __forceinline__ float acospi_q(float q) {
+#if VR_ABLATE & 2
+  return fmaf(q, -0.5f, 0.5f);  // diagnostic: the angle's cost removed (wrong image)
+#endif
 #if VR_FAST_ACOS
   const float t = fabsf(q);
 #if VR_ACOS_LITERALS
@@ -558,8 +561,13 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
         const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
         const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
         float light0, light1;
+#if VR_ABLATE & 1  // diagnostic: the LUT fetch's cost removed (wrong image)
+        light0 = beta0 + gamma0 + la.w;
+        light1 = beta1 + gamma1 + la.w;
+#else
         fetch_small2(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
                      axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
+#endif
         const float rl0 = refl * light0;
         ir = fmaf(rl0 * L0.cr, P.color[0], ir);
         ig = fmaf(rl0 * L0.cg, P.color[1], ig);
