@@ -1399,6 +1399,28 @@ int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream
   return VR_OK;
 }
 
+// Group streams are never destroyed.  Events recorded on them (replica copies, group renders) live on
+// after the group is deleted -- in the reader lists of buffers that stay bound, pooled or retired --
+// and a later query of such an event reads the runtime's stream object: destroyed, that read gave
+// spurious stream-capture errors (hipErrorCapturedEvent / hipErrorStreamCaptureUnsupported from
+// unrelated calls, intermittently).  A deleted group's streams wait here for the next group.
+std::map<int, std::vector<hipStream_t>> &idle_streams() {
+  static std::map<int, std::vector<hipStream_t>> m;
+  return m;
+}
+hipError_t take_stream(int dev, hipStream_t *s) {  // dev is current
+  std::vector<hipStream_t> &v = idle_streams()[dev];
+  if (!v.empty()) {
+    *s = v.back();
+    v.pop_back();
+    return hipSuccess;
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+void give_stream(int dev, hipStream_t s) {  // s is idle
+  if (s) idle_streams()[dev].push_back(s);
+}
+
 void delete_children(vr_context *h) {
   for (vr_context *c : h->children) {
     DeviceGuard dg(c->device);
@@ -1411,7 +1433,7 @@ void delete_children(vr_context *h) {
     if (c->gdone) (void)hipEventDestroy(c->gdone);
     for (hipEvent_t e : c->tev)
       if (e) (void)hipEventDestroy(e);
-    if (c->gstream) (void)hipStreamDestroy(c->gstream);
+    give_stream(c->device, c->gstream);
     delete c;
   }
   h->children.clear();
@@ -1538,7 +1560,7 @@ int vr_new_multi(const int32_t *devices, int32_t n, vr_context **out) {
     c->device = devices[i];
     c->parent = h;
     h->children.push_back(c);
-    VR_HIP(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+    VR_HIP(take_stream(c->device, &c->gstream));
     VR_HIP(hipEventCreateWithFlags(&c->gdone, hipEventDisableTiming));
   }
   g_contexts.insert(h);
