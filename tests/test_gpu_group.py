@@ -175,3 +175,34 @@ def test_group_mem_info_lists_every_device(monkeypatch, counter_clock):
     assert txt.count("Emission:") == 3 and "(replica)" in txt, txt
     assert "last launch (ms): n/a" not in txt, txt
     r.delete()
+
+
+def test_groups_created_and_deleted_in_turn(monkeypatch, counter_clock):
+    """Events recorded on a group's streams (replica copies, part renders) outlive the group: the
+    buffers that read them stay bound, pooled or retired with the events in their reader lists, and
+    later syncs and renders query them (vr_capi.hip idle_streams: group streams are pooled, never
+    destroyed).  Groups of 2-4 devices are created, render two frames (data change between) and are
+    deleted, in turn with one-device renders that reuse the pool; every image equals the first
+    one-device render of its data."""
+    monkeypatch.setenv("VR_GROUP_REPLICATE", "1")
+    data = [O.shell_volume(40), np.asfortranarray(O.shell_volume(40)[::-1] * np.float32(0.8))]
+
+    def two_frames(devices):
+        if devices:
+            monkeypatch.setenv("VR_DEVICES", devices)
+        else:
+            monkeypatch.delenv("VR_DEVICES", raising=False)
+        r = _scene(vr.VolumeRender(), vr.Volume(data[0]))
+        out = [r.render()]
+        r.VolumeEmission.Data = data[1]
+        out.append(r.render())
+        monkeypatch.delenv("VR_DEVICES", raising=False)
+        r.delete()
+        return out
+
+    ref = two_frames(None)
+    assert ref[0].max() > 0 and ref[1].max() > 0
+    for devices in ("0,0", None, "0,0,0,0", "0,0,0", None, "0,0"):
+        got = two_frames(devices)
+        for k in range(2):
+            assert np.array_equal(got[k].view(np.uint32), ref[k].view(np.uint32)), (devices, k)
