@@ -68,6 +68,7 @@ hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipSt
 hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
+hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
@@ -204,7 +205,14 @@ struct DevBuf {
   // multi-device group (vr_new_multi): its copies on the other devices, and the version each copies
   std::map<int, std::shared_ptr<DevBuf>> replicas;
   std::map<int, uint64_t> replica_of;
-  ~DevBuf() { vr_host::pooled_free(ptr, bytes, device, std::move(readers)); }
+  // the illumination LUT (small textures bound to the LUT slot): its z-paired copy (zpair_kernel),
+  // from which the fast shading's lookups take two 16-byte loads per light instead of four 8-byte
+  float *zpair = nullptr;
+  uint64_t zpair_bytes = 0;
+  ~DevBuf() {
+    if (zpair) vr_host::pooled_free(zpair, zpair_bytes, device, vr_host::Readers(readers));
+    vr_host::pooled_free(ptr, bytes, device, std::move(readers));
+  }
 };
 using BufPtr = std::shared_ptr<DevBuf>;
 
@@ -323,6 +331,30 @@ bool env_flag_off(const char *name) {
 // nothing else holds it and no launch still reads it; otherwise a fresh buffer is taken and the old
 // one is freed when its last launch completes (a render of the previous frame may be in flight on
 // another stream while this frame's volumes upload, vr_resources.h).
+// The LUT's z-paired copy (DevBuf::zpair) for a texture small enough for fetch_small and not a
+// single voxel; rebuilt with every upload into the buffer (the buffer's readers have completed).
+// VR_NO_ZPAIR=1: none (the fast kernels then shade without the tame path, an A/B switch).
+void build_zpair(DevBuf *b, hipStream_t s) {
+  const uint64_t padded = (b->dims[0] + 2) * (b->dims[1] + 2) * (b->dims[2] + 2);
+  const bool want = padded < (1ull << 22) && !(b->dims[0] == 1 && b->dims[1] == 1 && b->dims[2] == 1) &&
+                    !env_flag("VR_NO_ZPAIR");
+  if (!want) {
+    if (b->zpair) vr_host::pooled_free(b->zpair, b->zpair_bytes, b->device, vr_host::Readers(b->readers));
+    b->zpair = nullptr;
+    b->zpair_bytes = 0;
+    return;
+  }
+  if (b->zpair_bytes != 2 * padded * sizeof(float)) {
+    if (b->zpair) vr_host::pooled_free(b->zpair, b->zpair_bytes, b->device, vr_host::Readers(b->readers));
+    b->zpair = nullptr;
+    b->zpair_bytes = 2 * padded * sizeof(float);
+    VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->zpair), b->zpair_bytes, b->device));
+  }
+  const uint32_t pxy = (uint32_t)((b->dims[0] + 2) * (b->dims[1] + 2));
+  VR_HIP(vr::launch_zpair(b->ptr, b->zpair, (uint32_t)padded, pxy, s));
+  VR_HIP(hipStreamSynchronize(s));
+}
+
 void sync_volume(vr_context *h, int tex, int slot) {
   g_tex.bind[tex].reset();
   const VolRec &v = h->vol[slot];
@@ -349,6 +381,7 @@ void sync_volume(vr_context *h, int tex, int slot) {
                     b->ptr, &st));
     b->nonfinite = st.nonfinite != 0;
     b->maxabs = st.maxabs;
+    if (tex == T_LIGHT) build_zpair(b.get(), U.stream);
   }
   b->version = next_version();
   b->src_data = v.data;
@@ -502,6 +535,7 @@ vr::DevTex dev_tex(const BufPtr &b) {
     t.fpx4 = 4.f * (float)t.px;
     t.fpxy4 = 4.f * (float)t.pxy;
     t.fbase4 = 4.f * (float)(t.pxy + t.px + 1);
+    t.zp = t.small ? b->zpair : nullptr;
   }
   return t;
 }
@@ -691,7 +725,7 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
   }
   {
     const bool re_ok = P.re_is_em || (P.re.p && P.re.one);
-    const bool lut_ok = g_tex.lights.empty() || (P.lut.p && P.lut.small && !P.lut.one);
+    const bool lut_ok = g_tex.lights.empty() || (P.lut.p && P.lut.small && !P.lut.one && P.lut.zp);
     P.tame = (P.skip_empty && P.eds_finite && P.small_x && re_ok && lut_ok && !env_flag("VR_NO_TAME")) ? 1 : 0;
     P.re_mask = P.re_is_em ? 0xffffffffu : 0u;
   }

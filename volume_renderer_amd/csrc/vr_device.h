@@ -22,6 +22,7 @@ struct DevTex {
   int32_t small;  // padded size < 2^22 voxels: byte offsets are exact in fp32 (fetch_small)
                   // (VR_NO_SMALL_LUT=1 forces the general path, a test switch)
   float fpx4, fpxy4, fbase4;  // 4*px, 4*pxy, 4*(pxy+px+1): byte-offset terms for fetch_small
+  const float *zp;  // small textures: the z-paired copy (vr_kernels.hip zpair_kernel), or null
 };
 
 // One light in kernel order (position reversed from MATLAB, render.cpp:167-168).

@@ -575,6 +575,22 @@ hipError_t launch_pad_planes(const float *src, int64_t z0, int32_t nx, int32_t n
   return hipGetLastError();
 }
 
+// The z-paired copy of a small padded texture (the illumination LUT, fetch_small_z): entry i holds
+// voxel i and its +z neighbour i + pxy (itself in the last plane, which no lookup's lower corner is
+// in), so one 16-byte load at entry i gives the x-pair of two consecutive planes.
+__global__ void zpair_kernel(const float *src, float *dst, uint32_t n, uint32_t pxy) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a = src[i], b = i + pxy < n ? src[i + pxy] : a;
+  reinterpret_cast<float2 *>(dst)[i] = make_float2(a, b);
+}
+
+hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(zpair_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, pxy);
+  return hipGetLastError();
+}
+
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s) {
   if (!n) return hipSuccess;
   uint64_t blocks = (n + 255) / 256;

@@ -19,6 +19,7 @@ __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 
 typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef float f4a8 __attribute__((ext_vector_type(4), aligned(8)));
 
 // One axis of the linear-filter address computation (normalized coords, clamp addressing):
 // pair base i' = clamp(floor(c*n - 0.5), -1, n-1) and the 8-bit weight.  The clamp runs on the
@@ -213,6 +214,42 @@ __device__ __forceinline__ void fetch_small2(const DevTex &t, const AxF &ax, con
     const float c01 = lerp(b01.x, b01.y, ax.w), c11 = lerp(b11.x, b11.y, ax.w);
     v1 = lerp(lerp(c00, c10, ay1.w), lerp(c01, c11, ay1.w), az1.w);
   }
+}
+// The same lookups from the texture's z-paired copy (DevTex::zp, entries {v(i), v(i + pxy)}): a
+// 16-byte load at entry i holds the x-pair of plane z and of plane z + 1, so one lookup is two row
+// loads (rows y and y + 1) where fetch_small takes four, and touches half the cache lines.  The
+// lerps are fetch_small's, in its order, on the same values: bit-identical.
+#ifndef VR_LUT_ZPAIR
+#define VR_LUT_ZPAIR 1
+#endif
+__device__ __forceinline__ float lerp_zrows(const f4a8 &r0, const f4a8 &r1, const AxF &ax, const AxF &ay,
+                                            const AxF &az) {
+  const float c00 = lerp(r0.x, r0.z, ax.w), c10 = lerp(r1.x, r1.z, ax.w);
+  const float c01 = lerp(r0.y, r0.w, ax.w), c11 = lerp(r1.y, r1.w, ax.w);
+  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
+  return lerp(c0, c1, az.w);
+}
+__device__ __forceinline__ float fetch_small_z(const DevTex &t, const AxF &ax, const AxF &ay, const AxF &az) {
+  const uint32_t o = (uint32_t)fmaf(az.fl, t.fpxy4, fmaf(ay.fl, t.fpx4, fmaf(ax.fl, 4.f, t.fbase4)));
+  const uint32_t o2 = o + o, px8 = t.px * 8u;  // entries are 8 bytes
+  const char *b = reinterpret_cast<const char *>(t.zp);
+  const f4a8 r0 = *reinterpret_cast<const f4a8 *>(b + o2);
+  const f4a8 r1 = *reinterpret_cast<const f4a8 *>(b + (o2 + px8));
+  return lerp_zrows(r0, r1, ax, ay, az);
+}
+__device__ __forceinline__ void fetch_small2_z(const DevTex &t, const AxF &ax, const AxF &ay0, const AxF &az0,
+                                               const AxF &ay1, const AxF &az1, float &v0, float &v1) {
+  const float ox = fmaf(ax.fl, 4.f, t.fbase4);
+  const uint32_t o0 = (uint32_t)fmaf(az0.fl, t.fpxy4, fmaf(ay0.fl, t.fpx4, ox));
+  const uint32_t o1 = (uint32_t)fmaf(az1.fl, t.fpxy4, fmaf(ay1.fl, t.fpx4, ox));
+  const uint32_t px8 = t.px * 8u;
+  const char *b = reinterpret_cast<const char *>(t.zp);
+  const f4a8 a0 = *reinterpret_cast<const f4a8 *>(b + (o0 + o0));
+  const f4a8 a1 = *reinterpret_cast<const f4a8 *>(b + (o0 + o0 + px8));
+  const f4a8 b0 = *reinterpret_cast<const f4a8 *>(b + (o1 + o1));
+  const f4a8 b1 = *reinterpret_cast<const f4a8 *>(b + (o1 + o1 + px8));
+  v0 = lerp_zrows(a0, a1, ax, ay0, az0);
+  v1 = lerp_zrows(b0, b1, ax, ay1, az1);
 }
 __device__ __forceinline__ Ax to_ax(const AxF &a) { return Ax{(int)a.fl, a.w}; }
 
@@ -565,8 +602,12 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
         light0 = beta0 + gamma0 + la.w;
         light1 = beta1 + gamma1 + la.w;
 #else
-        fetch_small2(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
-                     axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
+        if (TAME && VR_LUT_ZPAIR)  // the host binds a tame launch's LUT with its z-paired copy
+          fetch_small2_z(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
+                         axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
+        else
+          fetch_small2(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
+                       axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
 #endif
         const float rl0 = refl * light0;
         ir = fmaf(rl0 * L0.cr, P.color[0], ir);
@@ -607,8 +648,10 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
       const float beta = acospi_q(dlo * (rn * __builtin_amdgcn_rsqf(dot3(lo, lo))));
       const float gamma = acospi_q(dot3(lip, lop) * (rlip * __builtin_amdgcn_rsqf(dot3(lop, lop))));
-      const float rl = refl * (TAME ? fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
-                                                  axis_lut<true>(gamma, P.lut.fnz))
+      const float rl = refl * (TAME ? (VR_LUT_ZPAIR ? fetch_small_z(P.lut, la, axis_lut<true>(beta, P.lut.fny),
+                                                                   axis_lut<true>(gamma, P.lut.fnz))
+                                                    : fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
+                                                                  axis_lut<true>(gamma, P.lut.fnz)))
                                     : lut_light<true>(P.lut, la, beta, gamma));
       ir = fmaf(rl * L.cr, P.color[0], ir);
       ig = fmaf(rl * L.cg, P.color[1], ig);
