@@ -68,7 +68,7 @@ hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipSt
 hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
-hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
+hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s, uint32_t quad_px);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
@@ -344,14 +344,16 @@ void build_zpair(DevBuf *b, hipStream_t s) {
     b->zpair_bytes = 0;
     return;
   }
-  if (b->zpair_bytes != 2 * padded * sizeof(float)) {
+  const bool quad = env_flag("VR_LUT_QUAD");  // A/B: the yz-quad copy (a VR_LUT_ZPAIR=2 build reads it)
+  const uint64_t bytes = (quad ? 4 : 2) * padded * sizeof(float);
+  if (b->zpair_bytes != bytes) {
     if (b->zpair) vr_host::pooled_free(b->zpair, b->zpair_bytes, b->device, vr_host::Readers(b->readers));
     b->zpair = nullptr;
-    b->zpair_bytes = 2 * padded * sizeof(float);
+    b->zpair_bytes = bytes;
     VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->zpair), b->zpair_bytes, b->device));
   }
   const uint32_t pxy = (uint32_t)((b->dims[0] + 2) * (b->dims[1] + 2));
-  VR_HIP(vr::launch_zpair(b->ptr, b->zpair, (uint32_t)padded, pxy, s));
+  VR_HIP(vr::launch_zpair(b->ptr, b->zpair, (uint32_t)padded, pxy, s, quad ? (uint32_t)(b->dims[0] + 2) : 0u));
   VR_HIP(hipStreamSynchronize(s));
 }
 

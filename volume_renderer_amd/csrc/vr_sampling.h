@@ -229,6 +229,34 @@ __device__ __forceinline__ float lerp_zrows(const f4a8 &r0, const f4a8 &r1, cons
   const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
   return lerp(c0, c1, az.w);
 }
+#if VR_LUT_ZPAIR == 2
+// VR_LUT_ZPAIR 2 (A/B, with VR_LUT_QUAD=1 on the host): the yz-quad copy, entries {v(i), v(i + pxy),
+// v(i + px), v(i + px + pxy)}; one lookup = the entries of x and x + 1 (32 contiguous bytes)
+__device__ __forceinline__ float lerp_quads(const f4a8 &e0, const f4a8 &e1, const AxF &ax, const AxF &ay,
+                                            const AxF &az) {
+  const float c00 = lerp(e0.x, e1.x, ax.w), c10 = lerp(e0.z, e1.z, ax.w);
+  const float c01 = lerp(e0.y, e1.y, ax.w), c11 = lerp(e0.w, e1.w, ax.w);
+  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
+  return lerp(c0, c1, az.w);
+}
+__device__ __forceinline__ float fetch_small_z(const DevTex &t, const AxF &ax, const AxF &ay, const AxF &az) {
+  const uint32_t o = (uint32_t)fmaf(az.fl, t.fpxy4, fmaf(ay.fl, t.fpx4, fmaf(ax.fl, 4.f, t.fbase4)));
+  const char *b = reinterpret_cast<const char *>(t.zp) + 4u * o;
+  return lerp_quads(*reinterpret_cast<const f4a8 *>(b), *reinterpret_cast<const f4a8 *>(b + 16), ax, ay, az);
+}
+__device__ __forceinline__ void fetch_small2_z(const DevTex &t, const AxF &ax, const AxF &ay0, const AxF &az0,
+                                               const AxF &ay1, const AxF &az1, float &v0, float &v1) {
+  const float ox = fmaf(ax.fl, 4.f, t.fbase4);
+  const uint32_t o0 = (uint32_t)fmaf(az0.fl, t.fpxy4, fmaf(ay0.fl, t.fpx4, ox));
+  const uint32_t o1 = (uint32_t)fmaf(az1.fl, t.fpxy4, fmaf(ay1.fl, t.fpx4, ox));
+  const char *a = reinterpret_cast<const char *>(t.zp) + 4u * o0;
+  const char *b = reinterpret_cast<const char *>(t.zp) + 4u * o1;
+  const f4a8 a0 = *reinterpret_cast<const f4a8 *>(a), a1 = *reinterpret_cast<const f4a8 *>(a + 16);
+  const f4a8 b0 = *reinterpret_cast<const f4a8 *>(b), b1 = *reinterpret_cast<const f4a8 *>(b + 16);
+  v0 = lerp_quads(a0, a1, ax, ay0, az0);
+  v1 = lerp_quads(b0, b1, ax, ay1, az1);
+}
+#else
 __device__ __forceinline__ float fetch_small_z(const DevTex &t, const AxF &ax, const AxF &ay, const AxF &az) {
   const uint32_t o = (uint32_t)fmaf(az.fl, t.fpxy4, fmaf(ay.fl, t.fpx4, fmaf(ax.fl, 4.f, t.fbase4)));
   const uint32_t o2 = o + o, px8 = t.px * 8u;  // entries are 8 bytes
@@ -251,6 +279,7 @@ __device__ __forceinline__ void fetch_small2_z(const DevTex &t, const AxF &ax, c
   v0 = lerp_zrows(a0, a1, ax, ay0, az0);
   v1 = lerp_zrows(b0, b1, ax, ay1, az1);
 }
+#endif
 __device__ __forceinline__ Ax to_ax(const AxF &a) { return Ax{(int)a.fl, a.w}; }
 
 // The LUT value of one light (0 if the illumination texture is unbound).
