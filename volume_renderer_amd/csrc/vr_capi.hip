@@ -939,7 +939,10 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   if (!full) {  // short launch: every launch measured, ordered longest first by the previous one
     P.sched_full = 0;
     if (S.measured) {
-      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, 0u, 0u);
+      // VR_SCHED_SHORT_DIV=d (A/B): the heavy blocks (>= 1/d of the longest) first, the rest row-major
+      uint32_t div = 0;
+      if (const char *ev = std::getenv("VR_SCHED_SHORT_DIV")) div = (uint32_t)std::max(0, std::atoi(ev));
+      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, div, div ? wg_tail_arg(0) : 0u);
     } else {  // first launch of this shape: row-major order, durations recorded
       rc = vr::launch_iota(S.d_order, nb, stream);
       S.measured = true;
