@@ -131,3 +131,44 @@ def test_overlapping_readers_keep_the_volume_until_the_last_one():
     torch.cuda.synchronize()
     assert np.array_equal(o_big.cpu().numpy().view(np.uint32), want.view(np.uint32))
     vr.volumeRender("delete", h)
+
+
+def test_lookup_gradient_copy_built_on_another_stream():
+    """The interleaved copy of the lookup gradients (vr_capi.hip, TexUnit::gvec) is built by the first
+    launch that needs it, on that launch's stream.  A launch on another stream that finds it built
+    must wait for it (its ready event): here the building launch's stream is held back by a spin
+    kernel, and the second launch is issued right after it on another stream.  Both images equal
+    the serial render."""
+    n, res = 96, (300, 400)
+    H, W = res
+    data = O.shell_volume(n)
+    em = _stamped(data, 31)
+    re = _stamped(np.float32(1.0), 32)
+    lut = _stamped(vr.HenyeyGreenstein(32), 33)
+    g = vr.Volume(data).grad()
+    h = vr.volumeRender("new")
+
+    def sync(t0, order):
+        grads = [_stamped(g[j].Data, t0 + i) for i, j in enumerate(order)]
+        vr.volumeRender("sync_volumes", h, np.uint64(0), em, re, em, *grads)
+        return grads
+
+    keep = sync(40, (1, 0, 2))  # x and y swapped: other normals
+    first = vr.volumeRender("render", h, *_args(LIGHTS_A, lut, res))  # builds the copy of these
+    keep = sync(50, (0, 1, 2))  # the true gradients: the copy is stale (its memory may be pooled and reused)
+    ra, kp = mex.render_args(*_args(LIGHTS_A, lut, res))
+    a, b = (torch.cuda.Stream() for _ in range(2))
+    oa = torch.empty(3 * W * H, dtype=torch.float32, device="cuda")
+    ob = torch.empty_like(oa)
+    with torch.cuda.stream(a):
+        torch.cuda._sleep(100_000_000)
+    mex.render_device(h, ra, oa.data_ptr(), None, 0, a.cuda_stream)  # rebuilds the copy after the spin
+    mex.render_device(h, ra, ob.data_ptr(), None, 0, b.cuda_stream)  # finds it built
+    torch.cuda.synchronize()
+    ref = vr.volumeRender("render", h, *_args(LIGHTS_A, lut, res))
+    assert ref.max() > 0 and not np.array_equal(ref, first)
+    want = ref.reshape(-1, order="F").view(np.uint32)
+    assert np.array_equal(oa.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(ob.cpu().numpy().view(np.uint32), want)
+    del keep, kp
+    vr.volumeRender("delete", h)

@@ -288,7 +288,11 @@ struct TexUnit {
 };
 
 std::mutex g_mu;
-TexUnit g_tex;
+// The module state and the resource lists of vr_resources.h are never destroyed: at process exit
+// their destructors would run in an order unrelated to their use (a binding's buffer returning its
+// memory to an already destroyed pool, events destroyed after the runtime's own teardown) -- the
+// process exit releases the device memory anyway.
+TexUnit &g_tex = *new TexUnit();
 uint64_t g_version = 0;
 uint64_t next_version() { return ++g_version; }
 std::set<vr_context *> g_contexts;
@@ -773,7 +777,10 @@ void bind_reads(LaunchRec &L) {
       L.reads.push_back(b);
     }
   for (const auto &kv : g_tex.gvec)
-    if (kv.second.buf && kv.first == L.device) L.reads.push_back(kv.second.buf);
+    if (kv.second.buf && kv.first == L.device) {
+      wait_ready(kv.second.buf, L.stream);  // built by a launch on another stream, maybe still running
+      L.reads.push_back(kv.second.buf);
+    }
 }
 void stage_frame(LaunchRec &L, vr::RenderParams &P, const std::vector<vr::DevLight> &lights) {
   const void *d = nullptr;
@@ -1118,6 +1125,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       if (vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device) == hipSuccess) {
         for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);
         VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
+        // launches on other streams (another handle, a group's other children on this device) find
+        // the copy fresh and wait for this event before reading it (bind_reads)
+        VR_HIP(vr_host::record_event(stream, gv->ready));
         G.buf = gv;
         for (int i = 0; i < 3; ++i) {
           G.src[i] = src[i];
@@ -1444,7 +1454,7 @@ int group_render(vr_context *h, const vr_render_args *a, float *d_out, hipStream
 // spurious stream-capture errors (hipErrorCapturedEvent / hipErrorStreamCaptureUnsupported from
 // unrelated calls, intermittently).  A deleted group's streams wait here for the next group.
 std::map<int, std::vector<hipStream_t>> &idle_streams() {
-  static std::map<int, std::vector<hipStream_t>> m;
+  static std::map<int, std::vector<hipStream_t>> &m = *new std::map<int, std::vector<hipStream_t>>();
   return m;
 }
 hipError_t take_stream(int dev, hipStream_t *s) {  // dev is current

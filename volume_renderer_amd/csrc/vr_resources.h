@@ -106,7 +106,7 @@ struct Retired {
 };
 
 inline std::vector<Retired> &retired() {
-  static std::vector<Retired> r;
+  static std::vector<Retired> &r = *new std::vector<Retired>();  // never destroyed (see g_tex)
   return r;
 }
 
@@ -157,7 +157,7 @@ struct Pooled {
 constexpr size_t POOL_MIN = 1ull << 20, POOL_MAX = 64ull << 30;
 
 inline std::vector<Pooled> &pool() {
-  static std::vector<Pooled> p;
+  static std::vector<Pooled> &p = *new std::vector<Pooled>();  // never destroyed (see g_tex)
   return p;
 }
 
@@ -258,7 +258,7 @@ struct ConstRing {
 };
 
 inline std::map<int, ConstRing> &rings() {
-  static std::map<int, ConstRing> r;
+  static std::map<int, ConstRing> &r = *new std::map<int, ConstRing>();  // never destroyed
   return r;
 }
 
@@ -521,7 +521,7 @@ struct Uploader {
 };
 
 inline std::map<int, Uploader> &uploaders() {
-  static std::map<int, Uploader> u;
+  static std::map<int, Uploader> &u = *new std::map<int, Uploader>();  // never destroyed
   return u;
 }
 
