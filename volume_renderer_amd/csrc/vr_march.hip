@@ -267,7 +267,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     }
     float refl;
     if constexpr (TAME) {  // the emission sample or the single voxel, selected by a 32-bit mask (v_bfi)
-      const float v = P.re.p[0];
+      const float v = voxel0(P.re.p);
       const uint32_t m = P.re_mask;
       refl = P.fr * __uint_as_float((__float_as_uint(em_s) & m) | (__float_as_uint(fmaf(0.5f, v - v, v)) & ~m));
     } else {

@@ -554,6 +554,21 @@ __device__ __forceinline__ float opacity(float a, float tstep, bool small = fals
 // SURVEY.md 8c, about 10 % faster at the metric configuration.
 // TAME (vr_march.hip sample_at): the launch's LUT, if it has lights, is a bound grid of fewer than
 // 2^22 padded voxels (RenderParams::tame), so only the fetch_small path is compiled.
+// The frame's light list through the constant address space: the list never changes during a launch,
+// so its (wave-uniform) loads are scalar loads in every kernel -- through a generic pointer the
+// compiler keeps them scalar only where no store of the kernel might alias them (in the slab kernel,
+// whose resume-point stores are inside the march, they became vector loads, 3 per light pair).
+__device__ __forceinline__ DevLight light_at(const RenderParams &P, int i) {
+  typedef const __attribute__((address_space(4))) DevLight *cptr;
+  const cptr q = (cptr)P.lights + i;  // generic -> constant: an address-space cast
+  return DevLight{q->px, q->py, q->pz, q->cr, q->cg, q->cb};
+}
+// The same for the voxel of a single-voxel texture (the tame reflection term).
+__device__ __forceinline__ float voxel0(const float *p) {
+  typedef const __attribute__((address_space(4))) float *cptr;
+  return ((cptr)p)[0];
+}
+
 template <bool FAST, bool TAME = false>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib) {
@@ -579,7 +594,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     }
     const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
     for (int i = 0; i < P.num_lights; ++i) {
-      const DevLight L = P.lights[i];
+      const DevLight L = light_at(P, i);
       const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
       const float dlo = dot3(lo, n);
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
@@ -616,7 +631,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
       // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
       for (; i + 1 < P.num_lights; i += 2) {
-        const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+        const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
         const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
         const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
         const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
@@ -649,7 +664,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       }
     }
     if constexpr (!TAME) for (; i + 1 < P.num_lights; i += 2) {
-      const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+      const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
       const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
       const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
       const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
@@ -671,7 +686,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       ib = fmaf(rl1 * L1.cb, P.color[2], ib);
     }
     if (i < P.num_lights) {
-      const DevLight L = P.lights[i];
+      const DevLight L = light_at(P, i);
       const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
       const float dlo = dot3(lo, n);
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
@@ -716,7 +731,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     // accumulation in light order, exactly as the reference's sequential loop
     int i = 0;
     for (; i + 1 < P.num_lights; i += 2) {
-      const DevLight L0 = P.lights[i], L1 = P.lights[i + 1];
+      const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
       const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);  // lightOut
       const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
       const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
@@ -754,7 +769,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       ib = fmaf(rl1 * L1.cb, P.color[2], ib);
     }
     if (i < P.num_lights) {
-      const DevLight L = P.lights[i];
+      const DevLight L = light_at(P, i);
       const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
       const float dlo = dot3(lo, n);
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
