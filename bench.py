@@ -315,6 +315,11 @@ def main():
             result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
                                              "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
 
+    if rank == 0 and world == 1:  # the frame's identity, also without the CPU baseline (A/B runs)
+        import hashlib
+        result["image_sha256"] = hashlib.sha256(
+            np.ascontiguousarray(out_local[: 3 * W * H].view(3, W, H).cpu().numpy()).tobytes()).hexdigest()
+
     # ---- CPU baseline: the oracle's sources at -O3 (C, OpenMP) on a column sample of the frame -----
     if rank == 0 and world == 1 and host_vol is not None:
         result["cpu_baseline"], result["parity_sampled_columns"] = cpu_baseline(

@@ -95,6 +95,9 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 #ifndef VR_SCHED_TAIL_PCT
 #define VR_SCHED_TAIL_PCT 60  // heavy-first only when the longest block >= this % of the packed frame
 #endif
+#ifndef VR_SCHED_SHIFT
+#define VR_SCHED_SHIFT 0.0  // full frames: heavy blocks moved ahead by this many block rows x duration / longest
+#endif
 #ifndef VR_SCHED_REMEASURE
 #define VR_SCHED_REMEASURE 16  // full frames: block durations re-measured every this many launches
 #endif
@@ -238,6 +241,7 @@ struct vr_context {
     // full frames: the measured durations copied to the host (asynchronously, after the launch) to
     // decide whether the heaviest block would form a tail
     uint32_t *h_cost = nullptr;
+    uint32_t *h_order = nullptr;  // pinned: a host-computed order (VR_SCHED_SHIFT / VR_SCHED_ROWS)
     hipEvent_t copied = nullptr;
     bool copy_pending = false, decided = false, tail = false;
   };
@@ -732,7 +736,10 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
   {
     const bool re_ok = P.re_is_em || (P.re.p && P.re.one);
     const bool lut_ok = g_tex.lights.empty() || (P.lut.p && P.lut.small && !P.lut.one && P.lut.zp);
-    P.tame = (P.skip_empty && P.eds_finite && P.small_x && re_ok && lut_ok && !env_flag("VR_NO_TAME")) ? 1 : 0;
+    // (tstep > 0: the march's t only grows, which advance_k relies on)
+    const bool step_ok = std::isfinite(P.tstep) && P.tstep > 0.f;
+    P.tame = (P.skip_empty && P.eds_finite && P.small_x && re_ok && lut_ok && step_ok && !env_flag("VR_NO_TAME")) ? 1
+                                                                                                            : 0;
     P.re_mask = P.re_is_em ? 0xffffffffu : 0u;
   }
   F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
@@ -824,6 +831,7 @@ void free_schedules(vr_context *h) {
     if (kv.second.d_cost) (void)hipFree(kv.second.d_cost);
     if (kv.second.d_order) (void)hipFree(kv.second.d_order);
     if (kv.second.h_cost) (void)hipHostFree(kv.second.h_cost);
+    if (kv.second.h_order) (void)hipHostFree(kv.second.h_order);
     if (kv.second.copied) (void)hipEventDestroy(kv.second.copied);
   }
   h->sched.clear();
@@ -969,6 +977,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     if (const char *ev = std::getenv("VR_SCHED_TAIL_PCT")) tail_pct = (uint32_t)std::max(0, std::atoi(ev));
     if (!S.h_cost) {
       if (hipHostMalloc(reinterpret_cast<void **>(&S.h_cost), nb * sizeof(uint32_t)) != hipSuccess ||
+          hipHostMalloc(reinterpret_cast<void **>(&S.h_order), nb * sizeof(uint32_t)) != hipSuccess ||
           hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
         return hipSuccess;  // no schedule
@@ -977,6 +986,12 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     // VR_SCHED_ROWS=1 (A/B): tile rows of workgroups in the order of their heaviest block, each row
     // in its own order -- the heavy band early, row-major neighbours still together
     const bool rows = env_flag("VR_SCHED_ROWS");
+    // VR_SCHED_SHIFT=r: row-major order with each block moved ahead by r block rows times its
+    // duration over the longest block's -- the heavy blocks start early enough to finish with the
+    // frame, row-major neighbours stay together (L2), and the frame ends on light blocks
+    double shift = VR_SCHED_SHIFT;
+    if (const char *ev = std::getenv("VR_SCHED_SHIFT")) shift = std::max(0.0, std::atof(ev));
+    if (rows) shift = 0.0;
     if (S.copy_pending && hipEventQuery(S.copied) == hipSuccess) {  // the last measurement arrived
       S.copy_pending = false;
       uint64_t sum = 0;
@@ -986,12 +1001,24 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
         mx = std::max(mx, S.h_cost[i]);
       }
       const uint64_t wg_slots = std::max<uint64_t>(1, (uint64_t)(device_wave_slots() / 16 * 6));
-      S.tail = rows || (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
+      S.tail = rows || shift > 0.0 || (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
       S.decided = true;
       S.order_stale = true;
-      if (rows) {  // workgroup wg is tile block (wg % nbx, wg / nbx) (vr_march.hip march_kernel)
-        const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
-        const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
+      // workgroup wg is tile block (wg % nbx, wg / nbx) (vr_march.hip march_kernel)
+      const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
+      const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
+      if (shift > 0.0 && mx > 0) {
+        std::vector<std::pair<double, uint32_t>> key(nb);
+        const double per = shift * (double)nbx / (double)mx;
+        for (uint32_t i = 0; i < nb; ++i) key[i] = {(double)i - per * (double)S.h_cost[i], i};
+        std::stable_sort(key.begin(), key.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        for (uint32_t i = 0; i < nb; ++i) S.h_order[i] = key[i].second;
+        // stream-ordered before every later launch; h_order is rewritten only after the next
+        // measurement's copy (later on this stream) has completed
+        VR_HIP(hipMemcpyAsync(S.d_order, S.h_order, nb * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+        S.order_stale = false;
+      }
+      if (rows) {
         const uint32_t nr = (nb + nbx - 1) / nbx;
         std::vector<std::pair<uint32_t, uint32_t>> rk(nr);
         for (uint32_t r = 0; r < nr; ++r) {
@@ -1168,6 +1195,12 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
                                         VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
       P.view_blocks = vfns[ki](P);
     }
+    // diagnostics (VR_SCHED_DUMP): a timed launch also records its blocks' start ticks
+    const char *dump = (P.wg_cost && P.sched_full != 2) ? std::getenv("VR_SCHED_DUMP") : nullptr;
+    uint32_t *d_start = nullptr;
+    if (dump && hipMalloc(reinterpret_cast<void **>(&d_start), (size_t)P.sched_blocks * 4) == hipSuccess)
+      P.wg_start = d_start;
+    (void)hipGetLastError();
     time_mark(h, 0, stream);
     VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
     time_mark(h, 1, stream);
@@ -1178,18 +1211,24 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       S.copy_pending = true;
       F.sched_copy = nullptr;
     }
-    if (P.wg_cost) {
-      if (const char *dump = std::getenv("VR_SCHED_DUMP")) {  // diagnostics: append block durations
-        std::vector<uint32_t> c(P.sched_blocks);
-        VR_HIP(hipMemcpyAsync(c.data(), P.wg_cost, c.size() * 4, hipMemcpyDeviceToHost, stream));
-        VR_HIP(hipStreamSynchronize(stream));
-        if (FILE *f = std::fopen(dump, "ab")) {
-          const uint32_t hdr[4] = {(uint32_t)K, (uint32_t)P.part, (uint32_t)P.num_parts, P.sched_blocks};
+    if (dump) {  // diagnostics: append block durations (and, in DUMP.start, their start ticks)
+      std::vector<uint32_t> c(P.sched_blocks), st(d_start ? P.sched_blocks : 0);
+      VR_HIP(hipMemcpyAsync(c.data(), P.wg_cost, c.size() * 4, hipMemcpyDeviceToHost, stream));
+      if (d_start) VR_HIP(hipMemcpyAsync(st.data(), d_start, st.size() * 4, hipMemcpyDeviceToHost, stream));
+      VR_HIP(hipStreamSynchronize(stream));
+      if (d_start) (void)hipFree(d_start);
+      const uint32_t hdr[4] = {(uint32_t)K, (uint32_t)P.part, (uint32_t)P.num_parts, P.sched_blocks};
+      if (FILE *f = std::fopen(dump, "ab")) {
+        std::fwrite(hdr, 4, 4, f);
+        std::fwrite(c.data(), 4, c.size(), f);
+        std::fclose(f);
+      }
+      if (d_start)
+        if (FILE *f = std::fopen((std::string(dump) + ".start").c_str(), "ab")) {
           std::fwrite(hdr, 4, 4, f);
-          std::fwrite(c.data(), 4, c.size(), f);
+          std::fwrite(st.data(), 4, st.size(), f);
           std::fclose(f);
         }
-      }
     }
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));

@@ -83,6 +83,7 @@ struct RenderParams {
   // block's duration in s_memrealtime ticks is stored to wg_cost[block] (null: not recorded)
   const uint32_t *wg_order;
   uint32_t *wg_cost;
+  uint32_t *wg_start;             // diagnostics (VR_SCHED_DUMP): each timed block's start tick (low 32 bits)
   uint32_t sched_blocks;          // length of wg_order / wg_cost (must equal the launch's grid)
   uint32_t sched_full;            // 0: a short launch's schedule (longest first, timed); full frames
                                   // (occupancy-capped kernel, heavy blocks first or row-major): 1 timed,

@@ -24,6 +24,20 @@
 #ifndef VR_MERGED_BOUNDS
 #define VR_MERGED_BOUNDS 1  // one wave-uniform slot test for the centre and the half-texel taps
 #endif
+#ifndef VR_WHOLE_BOX
+// 1: in a chunk whose whole tap box is staged (not partial; tame waves, not a slab), every tap of
+// every sample lies in the box by construction (plan_chunk: the box of all taps of the live rays'
+// next S samples, the drift of the rounded position additions in its halo), so the per-sample
+// merged slot test is not evaluated.  VR_CHECK_WHOLE=1 (diagnostic build): evaluated anyway, and a
+// sample it fails is reported with printf.
+#define VR_WHOLE_BOX 1
+#endif
+#ifndef VR_CHECK_WHOLE
+#define VR_CHECK_WHOLE 0
+#endif
+#if VR_CHECK_WHOLE
+static __device__ unsigned long long vr_whole_violations;  // (diagnostic build) samples the whole-box rule misses
+#endif
 #ifndef VR_BRANCHFREE_LEAP
 #define VR_BRANCHFREE_LEAP 1  // empty-chunk leap of K = 1 lanes without per-step branches
 #endif
@@ -130,7 +144,7 @@ struct ChunkStats {
 // absorption fetch, opacity, and for a lit, non-empty sample the gradient and the shading.  Returns
 // the premultiplied colour (r, g, b) and the opacity; `shaded` says whether shading ran.
 template <int MODE, bool AB_ALIAS, bool SHARE2, bool BIG, bool NANCHK>
-__device__ __forceinline__ void sample_at(const RenderParams &P, const float *L, const Box &B, bool staged,
+__device__ __forceinline__ void sample_at(const RenderParams &P, const float *L, const Box &B, bool staged, bool whole,
                                           const f3 pos, const f3 o, float &r, float &gg, float &b, float &alpha,
                                           bool &shaded) {
   const DevTex &E = P.em;
@@ -160,7 +174,10 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   }
   // centre cell in the slot; the gradient taps below differ from it along one axis only
   const int lx = slot_coord(ax.i, B.rx), ly = slot_coord(ay.i, B.ry), lz = slot_coord(az.i, B.rz);
-  const bool inx = in_box(lx, B.ex), iny = in_box(ly, B.ey), inz = in_box(lz, B.ez);
+  // (the per-axis box tests, evaluated where used: only the paths that are not wholly staged need them)
+#define inx in_box(lx, B.ex)
+#define iny in_box(ly, B.ey)
+#define inz in_box(lz, B.ez)
   const int ayz = lz * B.pxy + ly * B.px;  // slot word of (0, ly, lz)
   const int ac = ayz + lx;
   Cell C;  // the centre's partial sums, for the half-texel taps (valid where the centre is staged)
@@ -169,10 +186,23 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   // the centre cell is too (a - 1 >= 0 and a + 1 <= e - 2 put i in [0, e - 2]), so one wave-uniform
   // test serves the centre fetch and the gradient, with no per-lane branch on either
   bool full = false;
-  if constexpr (HALF_ONLY && VR_MERGED_BOUNDS)
-    full = __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
-                 (unsigned)(ly + (sy.hi ? 1 : 0) - 1) < (unsigned)(B.ey - 2) &&
-                 (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2));
+  if constexpr (HALF_ONLY && VR_MERGED_BOUNDS) {
+    if (VR_WHOLE_BOX && !VR_CHECK_WHOLE && whole) {
+      full = true;  // (wave-uniform) a whole box: every tap inside by construction
+    } else {
+      full = __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
+                   (unsigned)(ly + (sy.hi ? 1 : 0) - 1) < (unsigned)(B.ey - 2) &&
+                   (unsigned)(lz + (sz.hi ? 1 : 0) - 1) < (unsigned)(B.ez - 2));
+#if VR_CHECK_WHOLE
+      if (whole && !full && __lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) {
+        const unsigned long long c = atomicAdd(&vr_whole_violations, 1ull);
+        if (c < 8 || c % 100000 == 0)
+          printf("VR_CHECK_WHOLE: whole box misses a tap (#%llu): cell %d %d %d box %d %d %d + %d %d %d\n", c, ax.i,
+                 ay.i, az.i, B.rx, B.ry, B.rz, B.ex, B.ey, B.ez);
+      }
+#endif
+    }
+  }
   if constexpr (HALF_TAPS) {
     if (full) em_s = lds_tri_cell(L, B, ac, ax.w, ay.w, az.w, C);
     else if (staged && inx && iny && inz) em_s = lds_tri_cell(L, B, ac, ax.w, ay.w, az.w, C);
@@ -278,6 +308,9 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   r = fmaf(eds, P.color[0], ir) * alpha;
   gg = fmaf(eds, P.color[1], ig) * alpha;
   b = fmaf(eds, P.color[2], ib) * alpha;
+#undef inx
+#undef iny
+#undef inz
 }
 
 // Front-to-back compositing of one sample and the march recurrences of volumeRender_kernel.cu:
@@ -299,25 +332,43 @@ __device__ __forceinline__ void composite(const RenderParams &P, Ray &R, float r
   }
 }
 
-// Whether any lane of this lane's K-lane group has b set.
+// Whether any lane of this lane's K-lane group has b set (called by whole groups).  K = 2, 4: DPP
+// quad_perm swaps within the group (no 64-bit ballot arithmetic); K = 8: the ballot.
+#ifndef VR_GROUP_ANY_DPP
+#define VR_GROUP_ANY_DPP 1
+#endif
 template <int K>
 __device__ __forceinline__ bool group_any(bool b) {
-  const uint64_t m = __ballot(b);
-  const int base = (int)(__lane_id() & ~(uint32_t)(K - 1));
-  return ((m >> base) & ((1ull << K) - 1)) != 0ull;
+  if constexpr ((K == 2 || K == 4) && VR_GROUP_ANY_DPP) {
+    int v = b ? 1 : 0;
+    v |= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (K == 4) v |= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true);  // [2,3,0,1]: lane ^ 2
+    return v != 0;
+  } else {
+    const uint64_t m = __ballot(b);
+    const int base = (int)(__lane_id() & ~(uint32_t)(K - 1));
+    return ((m >> base) & ((1ull << K) - 1)) != 0ull;
+  }
 }
 
 // Composite the existing samples (a prefix of the K; exf = 1 where this lane's sample exists) of a
 // depth-lane group in order, every lane of the group alike; the ray stops at the first sum.a > thr
 // (volumeRender_kernel.cu:482).
-template <int K, int I>
+// ZF (tame waves): a missing sample is composited as its zeros, without the existence test -- an
+// exact no-op there: fma(1 - sum.a, 0, s) = s for the finite sums of a tame launch (never -0: they
+// start at +0 and an exact zero sum rounds to +0), and the exit test sees the unchanged sum.a,
+// which a live ray has already passed.  Saves the broadcast and test of exf per group lane.
+#ifndef VR_ZERO_FILL
+#define VR_ZERO_FILL 1
+#endif
+template <int K, int I, bool ZF = false>
 __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, float exf, float r, float gg, float b,
                                                 float alpha) {
   if constexpr (I < K) {
     const float ri = group_lane<K, I>(r), gi = group_lane<K, I>(gg), bi = group_lane<K, I>(b),
                 ai = group_lane<K, I>(alpha);
     // sample I of the group exists iff group lane I's does (the existing samples are a prefix)
-    if (group_lane<K, I>(exf) != 0.f && R.alive) {
+    if ((ZF || group_lane<K, I>(exf) != 0.f) && R.alive) {
       const float om = 1.f - R.sa;
       R.sr = fmaf(om, ri, R.sr);
       R.sg = fmaf(om, gi, R.sg);
@@ -325,7 +376,7 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
       R.sa = fmaf(om, ai, R.sa);
       if (R.sa > P.thr) R.alive = false;
     }
-    composite_group<K, I + 1>(P, R, exf, r, gg, b, alpha);
+    composite_group<K, I + 1, ZF>(P, R, exf, r, gg, b, alpha);
   }
 }
 
@@ -372,8 +423,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     bool staged, partial;
     Box B;
     int box_vol = 0;
+    bool edge = true;  // the box is clamped at a volume face (set by plan_chunk when it stages a whole box)
     plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B,
-                    COUNT ? &box_vol : nullptr);
+                    COUNT ? &box_vol : nullptr, &edge);
     bool inside = true;  // slab mode: every sample of this chunk lies in the slab
     if constexpr (SLAB) {
       // a chunk none of whose samples this slab owns is not staged: its samples only replay the
@@ -415,13 +467,18 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     }
     __builtin_amdgcn_wave_barrier();
     if (COUNT) ++(staged && !partial ? (empty ? C.leap : C.staged) : C.fall);
+    // wave-uniform (sample_at: VR_WHOLE_BOX), held as one scalar rather than a lane mask
+    const bool whole = __builtin_amdgcn_readfirstlane((!NANCHK && !SLAB && staged && !partial && !edge) ? 1 : 0) != 0;
 
     if (empty) {
+      // tame waves: one exit test after the S additions (advance_n; t only grows)
       if constexpr (K == 1) {
         if (COUNT || !VR_BRANCHFREE_LEAP) leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);  // exact counts
+        else if constexpr (!NANCHK) advance_n(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
         else advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
       } else {
-        advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        if constexpr (!NANCHK) advance_n(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        else advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
         R.alive = R.alive && group_any<K>(R.mine);
       }
       continue;
@@ -452,7 +509,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         }
         float r, gg, b, alpha;
         bool shaded;
-        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
+        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded);
         if (COUNT) {
           ++C.iter;
           C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
@@ -474,9 +531,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         }
         if (take) {
           bool shaded;
-          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, R.pos, R.o, r, gg, b, alpha, shaded);
+          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded);
         }
-        composite_group<K, 0>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
+        composite_group<K, 0, VR_ZERO_FILL && !NANCHK && !SLAB>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
         if (SLAB && !inside) {
           if (R.alive && group_any<K>(R.mine && !ex)) {  // left the slab still unfinished
             // the next slab resumes at the group's first sample beyond this one (samples of a
@@ -490,7 +547,10 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
             R.past = true;
           }
         }
-        advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to sample + K
+        if constexpr (!NANCHK && !SLAB)  // tame: t is non-decreasing (tstep > 0), one test after K steps
+          advance_k<K>(P, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        else
+          advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to sample + K
         R.alive = R.alive && group_any<K>(R.mine);
       }
     }
@@ -609,6 +669,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     if (threadIdx.x == 0) {
       const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
       P.wg_cost[wgo] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
+      if (P.wg_start) P.wg_start[wgo] = (uint32_t)clk0;
     }
   }
   if (COUNT) {

@@ -367,9 +367,10 @@ struct Bounce {
       for (size_t i = (size_t)w; i < np; i += (size_t)T) {
         const int b = (int)(i % NB);
         if (i >= (size_t)NB)  // the piece that last held buffer b has been issued ...
-          while (issued.load(std::memory_order_acquire) <= i - NB)
+          while (issued.load(std::memory_order_acquire) <= i - NB) {
             if (stop.load(std::memory_order_relaxed)) return;
-            else std::this_thread::yield();
+            std::this_thread::yield();
+          }
         (void)hipEventSynchronize(ev[b]);  // ... and its DMA has completed
         const size_t off = i * PIECE;
         std::memcpy(pinned + (size_t)b * PIECE, static_cast<const char *>(src) + off, std::min(PIECE, bytes - off));

@@ -24,6 +24,9 @@ namespace vr {
 #ifndef VR_STAGE_UNROLL
 #define VR_STAGE_UNROLL 4  // loads in flight per lane while staging
 #endif
+#ifndef VR_STAGE_NT
+#define VR_STAGE_NT 0  // 1 (A/B): staging loads with the non-temporal hint (L2 streaming policy)
+#endif
 #ifndef VR_CHUNK
 #define VR_CHUNK 32      // samples per staged chunk (halved while the box does not fit)
 #endif
@@ -189,9 +192,12 @@ __device__ __forceinline__ float fetch_at(const DevTex &t, const float *L, const
 // Padded index range [lo, hi] (inclusive) of the tap pairs of one axis for a coordinate range.
 // `off` includes the staging margin (RenderParams::tap_off): it bounds the drift between the
 // predicted end position fma(step, k, pos) and the k sequentially rounded pos += step additions.
-__device__ __forceinline__ void axis_range(float c0, float c1, float off, int n, int &lo, int &hi) {
+// `edge`: set when the range is clamped to the apron, i.e. some tap of the range is a clamped tap at a
+// volume face, whose voxels a box cannot hold (then only the per-sample slot test is exact).
+__device__ __forceinline__ void axis_range(float c0, float c1, float off, int n, int &lo, int &hi, bool &edge) {
   const float cmin = fminf(c0, c1) - off, cmax = fmaxf(c0, c1) + off;
   const int a = (int)floorf(cmin), b = (int)floorf(cmax);
+  edge = edge || a < -1 || b > n - 1;
   lo = min(max(a, -1), n - 1) + 1;
   hi = min(max(b, -1), n - 1) + 2;
 }
@@ -272,7 +278,10 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
 #pragma unroll
     for (int j = 0; j < VR_STAGE_UNROLL; ++j) {
       li[j] = l;
-      if (k0 + j < n) v[j] = *reinterpret_cast<const float *>(base + g);
+      if (k0 + j < n) {
+        const float *src = reinterpret_cast<const float *>(base + g);
+        v[j] = VR_STAGE_NT ? __builtin_nontemporal_load(src) : *src;
+      }
       l += l_row;
       g += g_row;
       y += per;
@@ -306,7 +315,7 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
 template <int CAP>
 __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, const f3 &pos, const f3 &step,
                                            float t, float tfar, int &S, bool &staged, bool &partial, Box &B,
-                                           int *vol_out = nullptr) {
+                                           int *vol_out = nullptr, bool *edge_out = nullptr) {
   const DevTex &E = P.em;
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
   const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
@@ -317,17 +326,18 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
   B = Box{0, 0, 0, 1, 1, 1, 1, 1};
   for (int attempt = 0;; ++attempt) {
     int lo[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, hi[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
+    bool edge = false;
     if (alive) {
       const float rem = (tfar - t) / tstep;  // samples left before the exit test fires
       const int s_eff = (rem < (float)S) ? max((int)rem + 2, 1) : S;
       const float k = (float)(s_eff - 1);
       const f3 pe = mk(fmaf(step.x, k, pos.x), fmaf(step.y, k, pos.y), fmaf(step.z, k, pos.z));
       axis_range(((pos.x - bmin.x) * bsc.x) * E.fnx - 0.5f, ((pe.x - bmin.x) * bsc.x) * E.fnx - 0.5f,
-                 P.tap_off[0], E.nx, lo[0], hi[0]);
+                 P.tap_off[0], E.nx, lo[0], hi[0], edge);
       axis_range(((pos.y - bmin.y) * bsc.y) * E.fny - 0.5f, ((pe.y - bmin.y) * bsc.y) * E.fny - 0.5f,
-                 P.tap_off[1], E.ny, lo[1], hi[1]);
+                 P.tap_off[1], E.ny, lo[1], hi[1], edge);
       axis_range(((pos.z - bmin.z) * bsc.z) * E.fnz - 0.5f, ((pe.z - bmin.z) * bsc.z) * E.fnz - 0.5f,
-                 P.tap_off[2], E.nz, lo[2], hi[2]);
+                 P.tap_off[2], E.nz, lo[2], hi[2], edge);
     }
     B.rx = wave_min(lo[0]);
     B.ry = wave_min(lo[1]);
@@ -348,6 +358,7 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
         }
       }
       staged = true;
+      if (edge_out) *edge_out = __any(edge);
       return;
     }
     if (attempt == VR_ATTEMPTS - 1) break;
@@ -403,6 +414,33 @@ __device__ __forceinline__ void advance(const RenderParams &P, int n, bool &aliv
     pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
     alive = alive && nsteps < P.max_steps && !(t > tfar);
   }
+}
+
+// advance() for a tame launch (tstep > 0, finite): the additions of n samples, then one exit test
+// (t only grows and nsteps only counts up, so the intermediate tests are implied by the last).
+__device__ __forceinline__ void advance_n(const RenderParams &P, int n, bool &alive, int32_t &nsteps, float &t,
+                                          float tfar, f3 &pos, const f3 &step) {
+  for (int k = 0; k < n; ++k) {
+    t += P.tstep;
+    pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
+  }
+  nsteps += n;
+  alive = alive && nsteps < P.max_steps && !(t > tfar);
+}
+
+// advance() by a compile-time count for a tame launch (tstep > 0, finite): t only grows and nsteps
+// only counts up, so the exit tests of the intermediate samples are implied by the last one's --
+// the same `alive`, with the same rounded additions, and one test instead of n.
+template <int N>
+__device__ __forceinline__ void advance_k(const RenderParams &P, bool &alive, int32_t &nsteps, float &t, float tfar,
+                                          f3 &pos, const f3 &step) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    t += P.tstep;
+    pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
+  }
+  nsteps += N;
+  alive = alive && nsteps < P.max_steps && !(t > tfar);
 }
 
 }  // namespace vr
