@@ -17,6 +17,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 
 #ifndef VR_MARCH_K
 #define VR_MARCH_K 1  // depth lanes of this object file (see below)
@@ -34,6 +35,9 @@
 #endif
 #ifndef VR_CHECK_WHOLE
 #define VR_CHECK_WHOLE 0
+#endif
+#ifndef VR_WHOLE_SPLIT
+#define VR_WHOLE_SPLIT 1  // K > 1: the sample loop compiled twice, for whole chunks and the others
 #endif
 #if VR_CHECK_WHOLE
 static __device__ unsigned long long vr_whole_violations;  // (diagnostic build) samples the whole-box rule misses
@@ -518,6 +522,10 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         composite(P, R, r, gg, b, alpha);
       }
     } else {
+      // WC: the chunk's box is whole (sample_at skips its slot test); a separate copy of the loop,
+      // so that the test and its flag are not carried through the samples of a whole chunk
+      auto samples = [&](auto wc) {
+      constexpr bool WC = decltype(wc)::value;
       for (int k = 0; k < S && R.alive; k += K) {
         float r = 0.f, gg = 0.f, b = 0.f, alpha = 0.f;
         bool ex = R.mine, take = R.mine;
@@ -531,7 +539,8 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         }
         if (take) {
           bool shaded;
-          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded);
+          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, WC || (!VR_WHOLE_SPLIT && whole), R.pos,
+                                                         R.o, r, gg, b, alpha, shaded);
         }
         composite_group<K, 0, VR_ZERO_FILL && !NANCHK && !SLAB>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
         if (SLAB && !inside) {
@@ -552,6 +561,14 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         else
           advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to sample + K
         R.alive = R.alive && group_any<K>(R.mine);
+      }
+      };
+      // (only the half-texel tap launch has the slot test that a whole chunk skips, sample_at)
+      if constexpr (VR_WHOLE_SPLIT && !NANCHK && !SLAB && VR_MARCH_FAST && MODE == 1 && SHARE2) {
+        if (whole) samples(std::true_type{});
+        else samples(std::false_type{});
+      } else {
+        samples(std::false_type{});
       }
     }
     __builtin_amdgcn_wave_barrier();
