@@ -5,7 +5,7 @@ RUN=${1:-r3bf}
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$RUN &&
 { timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/$RUN/tests.log 2>&1;
   rc=$?; echo "pytest rc=$rc" >> gpurun_out/$RUN/tests.log; [ $rc -eq 0 ]; } && tail -2 gpurun_out/$RUN/tests.log &&
-bash tools/ab_env_r3.sh gpurun_out/$RUN/ab.jsonl 3 "head=VR_LIB_PATH=build_ab/libvrhip_head.so" "tree=VR_X=1" &&
+bash tools/ab_env_r3.sh gpurun_out/$RUN/ab.jsonl 3 "head=VR_LIB_PATH=build_ab/libvrhip_head.so" "tree=VR_X=1" "pk=VR_LIB_PATH=build_ab/libvrhip_pk.so" &&
 python3 -c "
 import json,collections
 r=collections.defaultdict(list)

@@ -36,9 +36,14 @@
 #endif
 #if VR_WITH_K8
 #define VR_K8(k8, k4) k8
+#define VR_EXACT_K4(k4, k2) k4
 #else
 #define VR_K8(k8, k4) k4  // never selected: depth_lanes returns 8 only in a K = 8 build
+// The exact-arithmetic variant (a parity reference, VR_EXACT_SHADE=1) is built for K = 1, 2 only
+// (libvrhip.so size); exact_lanes caps its depth lanes at 2 -- the image is the same for every K.
+#define VR_EXACT_K4(k4, k2) k2
 #endif
+int exact_lanes(int K, bool fast) { return (fast || VR_WITH_K8) ? K : std::min(K, 2); }
 
 namespace vr {
 hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool big, bool share, hipStream_t s);
@@ -1177,13 +1182,14 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   bind_reads(L);
   stage_frame(L, P, g_tex.lights);
   if (march) {
-    const int K = P.steps ? 1 : depth_lanes(P);  // the counter variant exists for K = 1
+    const int K = P.steps ? 1 : exact_lanes(depth_lanes(P), P.fast_shade);  // the counter variant: K = 1
     set_chunk_halo(F, K);
     typedef hipError_t (*launch_fn)(const vr::RenderParams &, int, bool, bool, bool, hipStream_t);
     typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
     static const launch_fn fns[2][4] = {
-        {vr::exact::launch_march_k1, vr::exact::launch_march_k2, vr::exact::launch_march_k4,
-         VR_K8(vr::exact::launch_march_k8, vr::exact::launch_march_k4)},
+        {vr::exact::launch_march_k1, vr::exact::launch_march_k2,
+         VR_EXACT_K4(vr::exact::launch_march_k4, vr::exact::launch_march_k2),
+         VR_K8(vr::exact::launch_march_k8, vr::exact::launch_march_k2)},
         {vr::fast::launch_march_k1, vr::fast::launch_march_k2, vr::fast::launch_march_k4,
          VR_K8(vr::fast::launch_march_k8, vr::fast::launch_march_k4)}};
     const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
@@ -1307,11 +1313,13 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   int K = depth_lanes(P);
   P.part_cols = tile_cols;
   if (K > 4) K = 4;
+  K = exact_lanes(K, P.fast_shade);
   set_chunk_halo(F, K);
   P.slab_margin = P.tap_off[2] / P.em.fnz;  // bound of the chunk ownership test, normalized
   typedef hipError_t (*slab_fn)(const vr::RenderParams &, int, hipStream_t);
   static const slab_fn sfns[2][3] = {
-      {vr::exact::launch_march_slab_k1, vr::exact::launch_march_slab_k2, vr::exact::launch_march_slab_k4},
+      {vr::exact::launch_march_slab_k1, vr::exact::launch_march_slab_k2,
+       VR_EXACT_K4(vr::exact::launch_march_slab_k4, vr::exact::launch_march_slab_k2)},
       {vr::fast::launch_march_slab_k1, vr::fast::launch_march_slab_k2, vr::fast::launch_march_slab_k4}};
   LaunchRec L;
   L.stream = stream;
@@ -1878,7 +1886,8 @@ void launch_view_set(ViewSet &VS, int device, hipStream_t stream, vr_context *ti
   const vr::DevLight *d_lights = static_cast<const vr::DevLight *>(dl);
   typedef hipError_t (*views_fn)(const vr::RenderViews &, uint32_t, int, bool, hipStream_t);
   static const views_fn vfns[2][3] = {
-      {vr::exact::launch_march_views_k1, vr::exact::launch_march_views_k2, vr::exact::launch_march_views_k4},
+      {vr::exact::launch_march_views_k1, vr::exact::launch_march_views_k2,
+       VR_EXACT_K4(vr::exact::launch_march_views_k4, vr::exact::launch_march_views_k2)},
       {vr::fast::launch_march_views_k1, vr::fast::launch_march_views_k2, vr::fast::launch_march_views_k4}};
   time_mark(timer, 0, stream);
   size_t g0 = 0;
@@ -1887,7 +1896,7 @@ void launch_view_set(ViewSet &VS, int device, hipStream_t stream, vr_context *ti
     while (g1 < nvw && key(order[g1]) == key(order[g0])) ++g1;
     // depth lanes as for one view: the frame's own tail sets them, and K = 2 stays ahead of K = 1
     // per sample even at many waves per slot
-    const int K = std::min(depth_lanes(views[order[g0]]), 4);
+    const int K = exact_lanes(std::min(depth_lanes(views[order[g0]]), 4), views[order[g0]].fast_shade);
     vr::RenderViews V;
     std::memset(&V, 0, sizeof V);
     for (size_t k = g0; k < g1; ++k) {

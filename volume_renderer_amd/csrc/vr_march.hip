@@ -36,6 +36,9 @@
 #ifndef VR_CHECK_WHOLE
 #define VR_CHECK_WHOLE 0
 #endif
+#ifndef VR_ADAPTIVE_S
+#define VR_ADAPTIVE_S 1
+#endif
 #ifndef VR_WHOLE_SPLIT
 #define VR_WHOLE_SPLIT 1  // K > 1: the sample loop compiled twice, for whole chunks and the others
 #endif
@@ -421,6 +424,11 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     R.alive = group_any<K>(R.mine);
   }
 
+  // VR_ADAPTIVE_S: the first box attempt of a chunk is twice the length the wave's last chunk
+  // staged (its box grows little from one chunk to the next), and the shortest after a partial box,
+  // instead of always VR_CHUNK halved until it fits: fewer box reductions per chunk.  The samples
+  // are the same whatever the chunk length (the staging never changes a result).
+  int s0 = VR_CHUNK;
   while (__any(R.alive)) {
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
     int S;
@@ -429,7 +437,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     int box_vol = 0;
     bool edge = true;  // the box is clamped at a volume face (set by plan_chunk when it stages a whole box)
     plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B,
-                    COUNT ? &box_vol : nullptr, &edge);
+                    COUNT ? &box_vol : nullptr, &edge, s0);
+    if (VR_ADAPTIVE_S)
+      s0 = (staged && !partial) ? min(2 * S, (int)VR_CHUNK) : (int)(VR_CHUNK >> (VR_ATTEMPTS - 1));
     bool inside = true;  // slab mode: every sample of this chunk lies in the slab
     if constexpr (SLAB) {
       // a chunk none of whose samples this slab owns is not staged: its samples only replay the
@@ -588,7 +598,7 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 #ifndef VR_MARCH_MIN_EU
 #define VR_MARCH_MIN_EU 6
 #endif
-constexpr int march_min_eu(int cap, int sched) { return (cap <= 1664 && sched != 1) ? VR_MARCH_MIN_EU : 1; }
+constexpr int march_min_eu(int cap, int sched) { return (cap <= VR_LDS_CAP && sched != 1) ? VR_MARCH_MIN_EU : 1; }
 #ifndef VR_WG_WAVES
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif
@@ -828,7 +838,7 @@ hipError_t VR_CAT(launch_march_views_k, VR_MARCH_K)(const RenderViews &V, uint32
 #define VR_SLAB_MIN_EU VR_MARCH_MIN_EU
 #endif
 template <int K, int MODE, bool SH, int CAP, bool SCHED>
-__global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= 1664 && !SCHED) ? VR_SLAB_MIN_EU : 1) void march_slab_kernel(
+__global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= VR_LDS_CAP && !SCHED) ? VR_SLAB_MIN_EU : 1) void march_slab_kernel(
     const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];

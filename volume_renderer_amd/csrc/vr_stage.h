@@ -56,6 +56,30 @@ __device__ __forceinline__ int wave_reduce(int v) {
 __device__ __forceinline__ int wave_min(int v) { return wave_reduce<false>(v); }
 __device__ __forceinline__ int wave_max(int v) { return wave_reduce<true>(v); }
 
+// wave_reduce<false> of two int16 fields packed in one dword, component-wise (v_pk_min_i16): the
+// chunk box's six bounds in three reductions (plan_chunk, VR_PACKED_BOUNDS).
+typedef short vr_s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int pk_min(int a, int b) {
+  return __builtin_bit_cast(int, __builtin_elementwise_min(__builtin_bit_cast(vr_s2, a), __builtin_bit_cast(vr_s2, b)));
+}
+__device__ __forceinline__ int wave_min2(int v) {
+  v = pk_min(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xf, 0xf, false));  // row_ror:8
+  v = pk_min(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xf, 0xf, false));  // row_ror:4
+  v = pk_min(v, __builtin_amdgcn_update_dpp(v, v, 0x122, 0xf, 0xf, false));  // row_ror:2
+  v = pk_min(v, __builtin_amdgcn_update_dpp(v, v, 0x121, 0xf, 0xf, false));  // row_ror:1
+  const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = pk_min((int)p16[0], (int)p16[1]);
+  const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = pk_min((int)p32[0], (int)p32[1]);
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ int pk2(int lo16, int hi16) { return (lo16 & 0xffff) | (int)((uint32_t)hi16 << 16); }
+__device__ __forceinline__ int pk_lo(int v) { return (int)(short)(v & 0xffff); }
+__device__ __forceinline__ int pk_hi(int v) { return v >> 16; }
+#ifndef VR_PACKED_BOUNDS
+#define VR_PACKED_BOUNDS 1
+#endif
+
 #ifndef VR_RELOAD_TEX
 #define VR_RELOAD_TEX 0
 #endif
@@ -315,12 +339,12 @@ __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &
 template <int CAP>
 __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, const f3 &pos, const f3 &step,
                                            float t, float tfar, int &S, bool &staged, bool &partial, Box &B,
-                                           int *vol_out = nullptr, bool *edge_out = nullptr) {
+                                           int *vol_out = nullptr, bool *edge_out = nullptr, int s0 = VR_CHUNK) {
   const DevTex &E = P.em;
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
   const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
   const float tstep = P.tstep;
-  S = VR_CHUNK;
+  S = s0;  // the first attempt (VR_CHUNK, or the wave's guess from its last chunk: VR_ADAPTIVE_S)
   staged = false;
   partial = false;
   B = Box{0, 0, 0, 1, 1, 1, 1, 1};
@@ -339,12 +363,27 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
       axis_range(((pos.z - bmin.z) * bsc.z) * E.fnz - 0.5f, ((pe.z - bmin.z) * bsc.z) * E.fnz - 0.5f,
                  P.tap_off[2], E.nz, lo[2], hi[2], edge);
     }
-    B.rx = wave_min(lo[0]);
-    B.ry = wave_min(lo[1]);
-    B.rz = wave_min(lo[2]);
-    B.ex = wave_max(hi[0]) - B.rx + 1;
-    B.ey = wave_max(hi[1]) - B.ry + 1;
-    B.ez = wave_max(hi[2]) - B.rz + 1;
+    if (VR_PACKED_BOUNDS && E.nx < 16000 && E.ny < 16000 && E.nz < 16000) {
+      // padded bounds lie in [0, n + 1] (and the dead-lane sentinels are clamped to +-16383), so
+      // they fit int16 fields: lo x/y, lo z / -hi x, -hi y / -hi z, each pair in one reduction
+      const int c = 16383;
+      const int a = wave_min2(pk2(min(lo[0], c), min(lo[1], c)));
+      const int b = wave_min2(pk2(min(lo[2], c), min(-hi[0], c)));
+      const int d = wave_min2(pk2(min(-hi[1], c), min(-hi[2], c)));
+      B.rx = pk_lo(a);
+      B.ry = pk_hi(a);
+      B.rz = pk_lo(b);
+      B.ex = -pk_hi(b) - B.rx + 1;
+      B.ey = -pk_lo(d) - B.ry + 1;
+      B.ez = -pk_hi(d) - B.rz + 1;
+    } else {
+      B.rx = wave_min(lo[0]);
+      B.ry = wave_min(lo[1]);
+      B.rz = wave_min(lo[2]);
+      B.ex = wave_max(hi[0]) - B.rx + 1;
+      B.ey = wave_max(hi[1]) - B.ry + 1;
+      B.ez = wave_max(hi[2]) - B.rz + 1;
+    }
     B.px = VR_ODD_PITCH == 1 ? (B.ex | 1) : B.ex;
     B.pxy = VR_ODD_PITCH == 1 ? ((B.px * B.ey) | 1) : B.px * B.ey;
     if (vol_out) *vol_out = B.pxy * B.ez;
@@ -361,7 +400,7 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
       if (edge_out) *edge_out = __any(edge);
       return;
     }
-    if (attempt == VR_ATTEMPTS - 1) break;
+    if (S <= (VR_CHUNK >> (VR_ATTEMPTS - 1))) break;  // the shortest chunk did not fit either
     S >>= 1;
   }
 #if VR_PARTIAL
