@@ -595,8 +595,11 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 // frame 43.8 ms (10 KiB, 16 waves) -> 42.6 (6 KiB) -> 41.2 (6.5 KiB; 1704 floats: 5 workgroups,
 // 41.9) at K = 2.  A scheduled launch (few rounds, heavy waves first) keeps the uncapped allocation: its
 // longest waves share a SIMD with fewer others (one rank's share at P = 8: 7.2 ms vs 7.7 capped).
+// Round 3, after the whole-box changes (fewer instructions between the loads a wave waits for): 5
+// waves per SIMD with a 96-VGPR budget (no spills) beat 6 with 80 -- same box, three rounds,
+// 31.25-31.40 vs 31.64-31.90 ms; 5 waves with 7.9 KiB slots (2016 floats) 31.42-31.54 (r3bg).
 #ifndef VR_MARCH_MIN_EU
-#define VR_MARCH_MIN_EU 6
+#define VR_MARCH_MIN_EU 5
 #endif
 constexpr int march_min_eu(int cap, int sched) { return (cap <= VR_LDS_CAP && sched != 1) ? VR_MARCH_MIN_EU : 1; }
 #ifndef VR_WG_WAVES
@@ -835,7 +838,7 @@ hipError_t VR_CAT(launch_march_views_k, VR_MARCH_K)(const RenderViews &V, uint32
 // resume point is its start).
 // SH / SCHED as for march_kernel: the half-texel tap launch; the longest-first schedule.
 #ifndef VR_SLAB_MIN_EU
-#define VR_SLAB_MIN_EU VR_MARCH_MIN_EU
+#define VR_SLAB_MIN_EU 6  // the slab kernel keeps 6 waves per SIMD (5 measured no faster, r3ag)
 #endif
 template <int K, int MODE, bool SH, int CAP, bool SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= VR_LDS_CAP && !SCHED) ? VR_SLAB_MIN_EU : 1) void march_slab_kernel(
