@@ -1,9 +1,9 @@
 #!/bin/bash
 # round-3 pass bi: same-box A/B of the final build (5 waves per SIMD) against 4 waves per SIMD
-# (VR_MARCH_MIN_EU=4, 128-VGPR budget) and against 8 staging loads in flight per lane (VR_STAGE_UNROLL=8)
+# (dropped: at 84 VGPRs it builds the same kernel) and against 8 staging loads in flight per lane (VR_STAGE_UNROLL=8)
 RUN=${1:-r3bi}
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$RUN &&
-bash tools/ab_env_r3.sh gpurun_out/$RUN/ab.jsonl 3 "tree=VR_X=1" "eu4=VR_LIB_PATH=build_ab/libvrhip_eu4.so" \
+bash tools/ab_env_r3.sh gpurun_out/$RUN/ab.jsonl 3 "tree=VR_X=1" \
   "u8=VR_LIB_PATH=build_ab/libvrhip_u8.so" &&
 python3 -c "
 import json,collections
