@@ -35,8 +35,9 @@ def main():
         dt = np.diff(np.append(t, span))
         idle = float(np.sum((peak - act) * dt)) / (peak * span) if span else 0.0
         below = lambda f: float(np.sum(dt[act < f * peak])) / 1e5  # ms (10 ns ticks)
-        # the last time residency was at >= 90 % of peak: everything after it is the ramp-down
-        full = t[act >= 0.9 * peak]
+        # the end of the last interval at >= 90 % of peak residency: everything after it is the ramp-down
+        t_next = np.append(t[1:], span)
+        full = t_next[act >= 0.9 * peak]
         ramp = (span - int(full.max())) / 1e5 if full.size else span / 1e5
         order = np.argsort(-dur)
         res.append({
