@@ -155,6 +155,8 @@ def main():
     staged_by_s = [int(v) for v in steps_t[40:44].tolist()]
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # N > 1: the end of each frame's gather (+ assembly on rank 0), for the per-rank attribution
+    evg = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if world > 1 else None
 
     timed_kernels = {}  # march kernel instantiation -> timed frames that launched it
 
@@ -171,6 +173,8 @@ def main():
             if rank == 0:
                 mex.assemble_partitions(gathered.data_ptr(), W, H, args.block_cols, world, max_cols,
                                         full.data_ptr(), sptr)
+            if i is not None:  # the gather waits on the RCCL stream: this marks its end
+                evg[i].record(stream)
 
     for _ in range(args.warmup):
         frame()
@@ -188,6 +192,11 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
+    ranks = None
+    if world > 1:  # per-rank kernel and gather + assembly times, all-gathered to rank 0
+        from volume_renderer_amd import parallel
+        gath_ms = [b.elapsed_time(g) for (_, b), g in zip(ev, evg)]
+        ranks = parallel.rank_report(t_kernel_s * 1e3, sum(gath_ms) / len(gath_ms), world, rank, device=dev)
 
     # ---- extra pass (not `value`): independent frames round-robin on several streams ----------
     pipe_elapsed = None
@@ -311,6 +320,8 @@ def main():
                                    "mrays_s": round(rays * args.steps / pipe_elapsed / 1e6, 3),
                                    "what": "the same frames issued round-robin on several HIP streams "
                                            "(independent movie frames overlap their tails); not `value`"}
+        if ranks is not None:
+            result["ranks"] = ranks
         if sim is not None:
             result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
                                              "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}

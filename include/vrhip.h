@@ -94,8 +94,10 @@ int vr_new(vr_context **out);
  * the bound volumes to the other devices over xGMI (peer copies); 'render' (and vr_render_device
  * without a partition or counters) renders column part k of the frame (16-column blocks dealt
  * round-robin) on devices[k], gathers the parts to the primary with peer copies and assembles the
- * image there -- bit-identical to the one-device render.  Stereo, channels and slab launches of a
- * group use the primary only.  A device may repeat (a rehearsal on one GPU). */
+ * image there -- bit-identical to the one-device render.  vr_render_stereo and vr_render_channels on
+ * group handles split their fused launches across the devices the same way; vr_render_slab and a
+ * vr_render_device call with a partition or counters run on the primary only.  A device may repeat
+ * (a rehearsal on one GPU). */
 int vr_new_multi(const int32_t *devices, int32_t n, vr_context **out);
 
 /* 'delete' (render.cpp:72-79 -> ~MManager, mmanager.hxx:103-105).  Like the reference's
@@ -278,6 +280,15 @@ int vr_debug_slot_transition(const int32_t idx_in[3], int32_t sim_em_ab, int32_t
 
 /* Last error message of this thread ("" if none). */
 const char *vr_last_error(void);
+
+/* HIP errors the library did not return to a caller (process-wide; the reference ignores every CUDA
+ * error, common.h:43-47): errors of its own calls that it handled with a fallback (an optional
+ * buffer, a launch schedule, timing events, an already enabled peer mapping) and errors found
+ * pending in the calling thread's HIP error state at an API entry (raised elsewhere; a device fault
+ * found there fails that call with VR_ERR_DEVICE).  Every other HIP error fails the call that met
+ * it.  Returns how many since the library was loaded and writes the last (up to 32) into buf, one
+ * per line, newest last: "<kind>: <hipError name> (<code>) at <site>". */
+int64_t vr_hip_errors(char *buf, size_t buflen);
 
 /* The demangled name of the march kernel instantiation the last render launched (the process's
  * last staged-march launch), e.g. "vr::fast::march_kernel<2, 1, true, false, true, false, 1664, 0>":

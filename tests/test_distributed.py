@@ -74,6 +74,41 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _report_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank r reports kernel 10 + r ms, gather 1 + 0.5 r ms
+        rep = parallel.rank_report(10.0 + rank, 1.0 + 0.5 * rank, world, rank)
+        if rank == 0:
+            q.put(rep)
+        else:
+            assert rep is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_report_attributes_a_multi_gpu_frame():
+    """bench.py's per-rank report at N > 1 (parallel.rank_report), over gloo at world 2: every rank's
+    kernel and gather + assembly times reach rank 0 in rank order, with their max / min and the
+    number of ranks the collective saw."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rep = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert rep["ranks_seen"] == 2 and rep["backend"] == "gloo"
+    assert rep["kernel_ms_per_rank"] == [10.0, 11.0] and rep["kernel_ms_max"] == 11.0 and rep["kernel_ms_min"] == 10.0
+    assert rep["gather_assembly_ms_per_rank"] == [1.0, 1.5] and rep["gather_assembly_ms_rank0"] == 1.0
+    assert rep["kernel_imbalance"] == 1.1
+
+
 @pytest.mark.parametrize("world", [2])
 def test_partitioned_render_gathers_to_the_full_image(world):
     ref = _render()

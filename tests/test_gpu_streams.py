@@ -172,3 +172,71 @@ def test_lookup_gradient_copy_built_on_another_stream():
     assert np.array_equal(ob.cpu().numpy().view(np.uint32), want)
     del keep, kp
     vr.volumeRender("delete", h)
+
+
+# ---- HIP errors are reported by the call that met them, or logged (vr_resources.h, vr_hip_errors) --
+
+
+def _scene():
+    em = _stamped(O.shell_volume(64), 41)
+    re = _stamped(np.float32(1.0), 42)
+    lut = _stamped(vr.HenyeyGreenstein(16), 43)
+    h = vr.volumeRender("new")
+    vr.volumeRender("sync_volumes", h, np.uint64(0), em, re, em)
+    return h, lut, (em, re)
+
+
+def test_failed_launch_is_reported_by_its_call(monkeypatch):
+    """A deliberately invalid launch configuration (VR_INJECT_BAD_LAUNCH: 2048 work-items per
+    workgroup, which the runtime rejects before dispatch) fails the 'render' call that issued it with
+    VR_ERR_DEVICE and the HIP error's text -- it is neither swallowed nor left for a later call: the
+    next render is correct and nothing was consumed into the handled-error log."""
+    from volume_renderer_amd import _lib
+    h, lut, keep = _scene()
+    good = vr.volumeRender("render", h, *_args(LIGHTS_A, lut, (96, 128)))
+    assert good.max() > 0
+    n0, _ = _lib.hip_errors()
+    monkeypatch.setenv("VR_INJECT_BAD_LAUNCH", "1")
+    with pytest.raises(_lib.VrError) as ei:
+        vr.volumeRender("render", h, *_args(LIGHTS_A, lut, (96, 128)))
+    monkeypatch.delenv("VR_INJECT_BAD_LAUNCH")
+    assert ei.value.code == 4, ei.value  # VR_ERR_DEVICE
+    assert "march kernel launch" in str(ei.value), str(ei.value)
+    again = vr.volumeRender("render", h, *_args(LIGHTS_A, lut, (96, 128)))
+    assert np.array_equal(again.view(np.uint32), good.view(np.uint32))
+    n1, lines = _lib.hip_errors()
+    assert n1 == n0, lines
+    vr.volumeRender("delete", h)
+    del keep
+
+
+def _hip_runtime():
+    """The HIP runtime this process (torch, libvrhip) uses, as a ctypes library."""
+    import ctypes
+    for line in open("/proc/self/maps"):
+        path = line.split()[-1] if len(line.split()) >= 6 else ""
+        if "libamdhip64.so" in path:
+            return ctypes.CDLL(path)
+    pytest.skip("libamdhip64 not mapped")
+
+
+def test_error_pending_at_entry_is_logged():
+    """An error another caller left in the thread's HIP error state (here a hipSetDevice of a device
+    that does not exist) is logged by the next libvrhip entry -- 'pending at entry', with the entry's
+    name -- and consumed there, so the call itself and the ones after it proceed (it is no device
+    fault)."""
+    import ctypes
+    from volume_renderer_amd import _lib
+    h, lut, keep = _scene()
+    hip = _hip_runtime()
+    n0, _ = _lib.hip_errors()
+    assert hip.hipSetDevice(ctypes.c_int(4096)) != 0
+    img = vr.volumeRender("render", h, *_args(LIGHTS_A, lut, (96, 128)))
+    assert img.max() > 0
+    n1, lines = _lib.hip_errors()
+    assert n1 == n0 + 1, lines
+    assert "pending at entry" in lines[-1] and "vr_render" in lines[-1], lines[-1]
+    vr.volumeRender("render", h, *_args(LIGHTS_A, lut, (96, 128)))
+    assert _lib.hip_errors()[0] == n1
+    vr.volumeRender("delete", h)
+    del keep

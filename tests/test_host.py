@@ -35,6 +35,15 @@ def test_library_exports_every_declared_symbol():
     assert b"gfx950" in L.vr_version()
 
 
+def test_hip_error_log_reads_without_a_gpu():
+    """vr_hip_errors (the log of HIP errors the library handled or found pending, never dropped)
+    reads without touching the device: a count and well-formed lines."""
+    n, lines = _lib.hip_errors()
+    assert n >= 0 and len(lines) <= min(n, 32)
+    for l in lines:
+        assert re.match(r"^(handled|pending|pending at entry): hipError\w+ \(\d+\) at .+", l), l
+
+
 def test_library_is_built_for_gfx950_only():
     out = os.popen(f"strings -a {_lib.LIB_PATH} | grep -o 'amdgcn-amd-amdhsa--gfx[0-9a-z]*' | sort -u").read()
     assert "gfx950" in out and not re.search(r"gfx9[0-4]", out.replace("gfx950", ""))

@@ -14,4 +14,4 @@ for k in 1 2 4; do
 done
 wait
 hipcc --offload-arch=gfx950 -shared -o ../../build_ab/libvrhip_$1.so ../../build_ab/$1/*.o \
-  vr_capi.o vr_kernels.o vr_volume_ops.o vr_march_exact_k1.o vr_march_exact_k2.o vr_march_exact_k4.o
+  vr_capi.o vr_kernels.o vr_volume_ops.o vr_march_exact_k*.o

@@ -97,6 +97,7 @@ SIGNATURES = [
     ("vr_debug_slot_transition", c_int, [POINTER(c_int32), c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                          POINTER(c_int32), POINTER(c_int32)]),
     ("vr_last_error", c_char_p, []),
+    ("vr_hip_errors", c_int64, [c_char_p, c_size_t]),
     ("vr_last_march_kernel", c_int, [c_char_p, c_size_t]),
     ("vr_version", c_char_p, []),
 ]
@@ -129,3 +130,11 @@ def check(rc: int) -> None:
     if rc != VR_OK:
         msg = lib().vr_last_error().decode(errors="replace")
         raise VrError(rc, msg)
+
+
+def hip_errors() -> tuple[int, list[str]]:
+    """HIP errors the library handled or found pending at an API entry (vr_hip_errors): the count
+    since load and the last log lines, newest last."""
+    buf = ctypes.create_string_buffer(32 * 400)
+    n = lib().vr_hip_errors(buf, len(buf))
+    return int(n), [l for l in buf.value.decode(errors="replace").splitlines() if l]

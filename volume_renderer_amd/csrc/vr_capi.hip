@@ -73,7 +73,7 @@ hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipSt
 hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
-hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s, uint32_t quad_px);
+hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
@@ -140,10 +140,7 @@ int fail(int code, const std::string &msg) {
   return code;
 }
 
-struct HipError {
-  hipError_t e;
-  const char *what;
-};
+using vr_host::HipError;
 
 #define VR_HIP(call)                                 \
   do {                                               \
@@ -357,16 +354,18 @@ void build_zpair(DevBuf *b, hipStream_t s) {
     b->zpair_bytes = 0;
     return;
   }
-  const bool quad = env_flag("VR_LUT_QUAD");  // A/B: the yz-quad copy (a VR_LUT_ZPAIR=2 build reads it)
-  const uint64_t bytes = (quad ? 4 : 2) * padded * sizeof(float);
-  if (b->zpair_bytes != bytes) {
+  const uint64_t bytes = 2 * padded * sizeof(float);
+  if (!b->zpair || b->zpair_bytes != bytes) {
     if (b->zpair) vr_host::pooled_free(b->zpair, b->zpair_bytes, b->device, vr_host::Readers(b->readers));
     b->zpair = nullptr;
+    b->zpair_bytes = 0;
+    // (the size is recorded only once the allocation exists: a failed allocation leaves no buffer
+    // that a later upload of the same size would take for allocated)
+    VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->zpair), bytes, b->device));
     b->zpair_bytes = bytes;
-    VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->zpair), b->zpair_bytes, b->device));
   }
   const uint32_t pxy = (uint32_t)((b->dims[0] + 2) * (b->dims[1] + 2));
-  VR_HIP(vr::launch_zpair(b->ptr, b->zpair, (uint32_t)padded, pxy, s, quad ? (uint32_t)(b->dims[0] + 2) : 0u));
+  VR_HIP(vr::launch_zpair(b->ptr, b->zpair, (uint32_t)padded, pxy, s));
   VR_HIP(hipStreamSynchronize(s));
 }
 
@@ -944,9 +943,10 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
                 P.block_cols, F.mode, P.wide_slot, P.fast_shade, nb, (void *)stream, extra);
   vr_context::Schedule &S = h->sched[key];
   if (!S.d_cost && nb) {
-    if (hipMalloc(&S.d_cost, nb * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&S.d_order, nb * sizeof(uint32_t)) != hipSuccess) {
-      (void)hipGetLastError();
+    hipError_t e = hipMalloc(&S.d_cost, nb * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&S.d_order, nb * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      vr_host::consume(e, "hipMalloc (launch schedule; the launch runs unscheduled)");
       if (S.d_cost) (void)hipFree(S.d_cost);
       S.d_cost = nullptr;
       S.d_order = nullptr;
@@ -981,10 +981,11 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     uint32_t tail_pct = VR_SCHED_TAIL_PCT;
     if (const char *ev = std::getenv("VR_SCHED_TAIL_PCT")) tail_pct = (uint32_t)std::max(0, std::atoi(ev));
     if (!S.h_cost) {
-      if (hipHostMalloc(reinterpret_cast<void **>(&S.h_cost), nb * sizeof(uint32_t)) != hipSuccess ||
-          hipHostMalloc(reinterpret_cast<void **>(&S.h_order), nb * sizeof(uint32_t)) != hipSuccess ||
-          hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
+      hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&S.h_cost), nb * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_order), nb * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        vr_host::consume(e, "hipHostMalloc / hipEventCreate (full-frame schedule; none used)");
         return hipSuccess;  // no schedule
       }
     }
@@ -997,7 +998,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     double shift = VR_SCHED_SHIFT;
     if (const char *ev = std::getenv("VR_SCHED_SHIFT")) shift = std::max(0.0, std::atof(ev));
     if (rows) shift = 0.0;
-    if (S.copy_pending && hipEventQuery(S.copied) == hipSuccess) {  // the last measurement arrived
+    if (S.copy_pending && vr_host::query_done(S.copied, "hipEventQuery (schedule durations)")) {  // arrived
       S.copy_pending = false;
       uint64_t sum = 0;
       uint32_t mx = 0;
@@ -1036,11 +1037,12 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
         ord.reserve(nb);
         for (const auto &x : rk)
           for (uint32_t i = x.second * nbx; i < std::min(nb, (x.second + 1) * nbx); ++i) ord.push_back(i);
-        VR_HIP(hipMemcpy(S.d_order, ord.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice));
+        // (ordered on the launch stream, from the pinned order buffer, as the VR_SCHED_SHIFT order)
+        std::copy(ord.begin(), ord.end(), S.h_order);
+        VR_HIP(hipMemcpyAsync(S.d_order, S.h_order, nb * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
         S.order_stale = false;
       }
     }
-    (void)hipGetLastError();
     bool measure = !S.measured;
     if (S.measured && !S.copy_pending && ++S.frames >= every) measure = true;
     if (measure) {
@@ -1078,12 +1080,15 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
 // Launch timing for mem_info (the context's device must be current).
 void time_mark(vr_context *h, int which, hipStream_t stream) {
   if (!h->tev[0]) {
-    if (hipEventCreate(&h->tev[0]) != hipSuccess || hipEventCreate(&h->tev[1]) != hipSuccess) {
-      (void)hipGetLastError();
+    hipError_t e = hipEventCreate(&h->tev[0]);
+    if (e == hipSuccess) e = hipEventCreate(&h->tev[1]);
+    if (e != hipSuccess) {
+      vr_host::consume(e, "hipEventCreate (mem_info kernel timing; not timed)");
       return;
     }
   }
-  if (hipEventRecord(h->tev[which], stream) != hipSuccess) (void)hipGetLastError();
+  const hipError_t e = hipEventRecord(h->tev[which], stream);
+  if (e != hipSuccess) vr_host::consume(e, "hipEventRecord (mem_info kernel timing; not timed)");
   if (which == 1) h->timed = true;
 }
 
@@ -1154,7 +1159,8 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
       gv->bytes = n * 4 * sizeof(float);
-      if (vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device) == hipSuccess) {
+      const hipError_t ea = vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device);
+      if (ea == hipSuccess) {
         for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);
         VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
         // launches on other streams (another handle, a group's other children on this device) find
@@ -1166,7 +1172,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
           G.ver[i] = src[i]->version;
         }
       } else {
-        (void)hipGetLastError();
+        vr_host::consume(ea, "pooled_alloc (interleaved lookup gradient; three separate gathers instead)");
         gv->ptr = nullptr;
       }
     }
@@ -1204,11 +1210,16 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     // diagnostics (VR_SCHED_DUMP): a timed launch also records its blocks' start ticks
     const char *dump = (P.wg_cost && P.sched_full != 2) ? std::getenv("VR_SCHED_DUMP") : nullptr;
     uint32_t *d_start = nullptr;
-    if (dump && hipMalloc(reinterpret_cast<void **>(&d_start), (size_t)P.sched_blocks * 4) == hipSuccess)
-      P.wg_start = d_start;
-    (void)hipGetLastError();
+    if (dump) {
+      const hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_start), (size_t)P.sched_blocks * 4);
+      if (e == hipSuccess) P.wg_start = d_start;
+      else vr_host::consume(e, "hipMalloc (VR_SCHED_DUMP start ticks; not recorded)");
+    }
     time_mark(h, 0, stream);
-    VR_HIP(fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream));
+    {
+      const hipError_t e = fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream);
+      if (e != hipSuccess) throw HipError{e, "the march kernel launch (launch_march_k)"};
+    }
     time_mark(h, 1, stream);
     if (F.sched_copy) {  // a timed full frame: its block durations to the host, for the tail test
       vr_context::Schedule &S = *F.sched_copy;
@@ -1381,7 +1392,8 @@ void enable_peer(int a, int b) {
   if (hipDeviceCanAccessPeer(&ok, a, b) == hipSuccess && ok) {
     DeviceGuard dg(a);
     const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-    if (e != hipSuccess) (void)hipGetLastError();  // already enabled / unsupported: copies still work
+    // already enabled / unsupported: peer copies still work (through the host if need be)
+    if (e != hipSuccess) vr_host::consume(e, "hipDeviceEnablePeerAccess (group peer mapping)");
   }
 }
 
@@ -1535,17 +1547,12 @@ void delete_children(vr_context *h) {
   h->children.clear();
 }
 
-// An error left in this thread's HIP error state by an earlier caller (another library, a call of
-// ours whose error was handled) must not be reported by this call's checks: cleared at entry
-// (VR_TRACE_STALE=1 prints it).
-inline void clear_stale(const char *fn) {
-  const hipError_t e = hipGetLastError();
-  static const bool trace = env_flag("VR_TRACE_STALE");
-  if (e != hipSuccess && trace) std::fprintf(stderr, "VR_TRACE_STALE %s: %s\n", fn, hipGetErrorString(e));
-}
+// At entry, an error already in this thread's HIP error state (another library's, or an
+// asynchronous device fault) is logged, and a device fault fails the call (vr_host::check_pending):
+// this call's own checks then see only its own errors.
 #define VR_GUARD_BEGIN \
-  clear_stale(__func__); \
-  try {
+  try {                \
+    vr_host::check_pending(__func__);
 #define VR_GUARD_END                                                                             \
   }                                                                                              \
   catch (const HipError &e) {                                                                    \
@@ -1764,11 +1771,16 @@ int vr_mem_info(vr_context *h, char *buf, size_t buflen) {
       else os << "not resident (replicated at the next render)\n";
     }
     float ms = -1.f;
-    if (c->timed && hipEventQuery(c->tev[1]) == hipSuccess && hipEventElapsedTime(&ms, c->tev[0], c->tev[1]) == hipSuccess)
+    bool have = c->timed && vr_host::query_done(c->tev[1], "hipEventQuery (mem_info launch timing)");
+    if (have) {
+      const hipError_t e = hipEventElapsedTime(&ms, c->tev[0], c->tev[1]);
+      if (e != hipSuccess) vr_host::consume(e, "hipEventElapsedTime (mem_info launch timing)");
+      have = e == hipSuccess;
+    }
+    if (have)
       os << "\t\t\tlast launch (ms): " << ms << "\n";
     else
       os << "\t\t\tlast launch (ms): n/a\n";
-    (void)hipGetLastError();
   }
   const std::string s = os.str();
   if (buf && buflen) {
@@ -2345,9 +2357,18 @@ int vr_resize_device(const float *d_in, const uint64_t in_dims[3], const uint64_
     std::vector<std::vector<double>> w;
     std::vector<std::vector<int32_t>> idx;
     ~Temps() {  // stream-ordered frees after the passes, then the host data is released
-      for (void *t : dev) (void)hipFreeAsync(t, s);
-      (void)hipStreamSynchronize(s);
-      (void)hipGetLastError();
+      hipError_t e = hipSuccess;
+      for (void *t : dev) {
+        const hipError_t r = hipFreeAsync(t, s);
+        if (e == hipSuccess) e = r;
+      }
+      const hipError_t r = hipStreamSynchronize(s);
+      if (e == hipSuccess) e = r;
+      // (a destructor: not thrown -- a device fault stays pending for the next entry's check)
+      if (e != hipSuccess && !vr_host::device_fault(e)) {
+        (void)hipGetLastError();
+        vr_host::log_error(e, "handled", "vr_resize_device temporaries", true);
+      }
     }
   } temps{s, {}, {}, {}};
   temps.w.reserve(passes.size());
@@ -2433,6 +2454,19 @@ uint64_t vr_timestamp(void) {
 }
 
 const char *vr_last_error(void) { return g_last_error.c_str(); }
+
+int64_t vr_hip_errors(char *buf, size_t buflen) {
+  vr_host::ErrLog &L = vr_host::errlog();
+  std::lock_guard<std::mutex> g(L.mu);
+  if (buf && buflen) {
+    std::string s;
+    for (const std::string &l : L.lines) s += l + "\n";
+    const size_t n = std::min(buflen - 1, s.size());
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return (int64_t)L.count;
+}
 
 int vr_last_march_kernel(char *buf, size_t buflen) {
   std::lock_guard<std::mutex> lk(g_mu);

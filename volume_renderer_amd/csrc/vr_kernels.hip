@@ -585,19 +585,9 @@ __global__ void zpair_kernel(const float *src, float *dst, uint32_t n, uint32_t 
   reinterpret_cast<float2 *>(dst)[i] = make_float2(a, b);
 }
 
-// The yz-quad copy (VR_LUT_QUAD=1, A/B): entry i holds voxels i, i + pxy, i + px, i + px + pxy, so
-// one lookup is the two adjacent 16-byte entries of x and x + 1.
-__global__ void yzquad_kernel(const float *src, float *dst, uint32_t n, uint32_t px, uint32_t pxy) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  auto at = [&](uint32_t j) { return j < n ? src[j] : src[i]; };
-  reinterpret_cast<float4 *>(dst)[i] = make_float4(src[i], at(i + pxy), at(i + px), at(i + px + pxy));
-}
-
-hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s, uint32_t quad_px) {
+hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s) {
   if (!n) return hipSuccess;
-  if (quad_px) hipLaunchKernelGGL(yzquad_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, quad_px, pxy);
-  else hipLaunchKernelGGL(zpair_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, pxy);
+  hipLaunchKernelGGL(zpair_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, pxy);
   return hipGetLastError();
 }
 

@@ -965,10 +965,19 @@ static unsigned short_launch_lds_pad() {
   return pad;
 }
 
+// VR_INJECT_BAD_LAUNCH=1 (tests only): the march launch asks for 2048 work-items per workgroup, more
+// than a gfx950 workgroup holds, so the runtime rejects it before dispatch -- the reporting path of
+// a failed launch (tests/test_gpu_streams.py::test_failed_launch_is_reported_by_its_call).  Read
+// per launch.
+static bool inject_bad_launch() {
+  const char *ev = getenv("VR_INJECT_BAD_LAUNCH");
+  return ev && ev[0] == '1';
+}
+
 template <int MODE, bool AB, bool SH, int CAP>
 static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
   constexpr int K = VR_MARCH_K;
-  const dim3 blk(64 * VR_WG_WAVES);
+  const dim3 blk(inject_bad_launch() ? 2048 : 64 * VR_WG_WAVES);
   const bool sched = P.wg_order && P.wg_cost;
   // scheduled kernels: K > 1, fast variant only (otherwise the names below alias the SCHED 0 kernel)
   constexpr bool SCH = K > 1 && VR_MARCH_FAST;

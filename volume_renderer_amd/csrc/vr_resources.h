@@ -25,6 +25,8 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -36,6 +38,93 @@ hipError_t launch_pad_planes(const float *src, int64_t z0, int32_t nx, int32_t n
 }
 
 namespace vr_host {
+
+// ---- HIP errors: reported or logged, never dropped ------------------------------------------------
+// The reference's release build ignores every CUDA error (common.h:43-47).  Here every error a HIP
+// call of the library returns is either thrown to the API caller (HipError -> VR_ERR_DEVICE with
+// the call's text) or, where the library has a fallback for it (an optional buffer, a launch
+// schedule, a timing event, an already enabled peer mapping), consumed from the thread's HIP error
+// state by consume() and appended to a process-wide log that vr_hip_errors() returns.  An error
+// found pending at an API entry (raised outside the library, or an asynchronous device fault) is
+// logged and printed; a device fault fails the call that finds it (check_pending).
+struct HipError {
+  hipError_t e;
+  const char *what;
+};
+
+struct ErrLog {
+  std::mutex mu;
+  uint64_t count = 0;
+  std::vector<std::string> lines;  // the last MAX entries
+  static constexpr size_t MAX = 32;
+};
+inline ErrLog &errlog() {
+  static ErrLog &l = *new ErrLog();  // never destroyed (see g_tex)
+  return l;
+}
+inline void log_error(hipError_t e, const char *kind, const char *site, bool print) {
+  char buf[320];
+  std::snprintf(buf, sizeof buf, "%s: %s (%d) at %s", kind, hipGetErrorName(e), (int)e, site);
+  ErrLog &L = errlog();
+  std::lock_guard<std::mutex> g(L.mu);
+  ++L.count;
+  if (L.lines.size() == ErrLog::MAX) L.lines.erase(L.lines.begin());
+  L.lines.emplace_back(buf);
+  static const bool verbose = [] {
+    const char *ev = std::getenv("VR_TRACE_STALE");
+    return ev && ev[0] == '1';
+  }();
+  if (print || verbose) std::fprintf(stderr, "libvrhip: %s\n", buf);
+}
+
+// Errors after which the device (context) is unusable: a kernel fault, an illegal access.
+inline bool device_fault(hipError_t e) {
+  switch (e) {
+    case hipErrorIllegalAddress:
+    case hipErrorLaunchFailure:
+    case hipErrorLaunchTimeOut:
+    case hipErrorAssert:
+    case hipErrorContextIsDestroyed:
+    case hipErrorECCNotCorrectable:
+      return true;
+    default:
+      return false;
+  }
+}
+
+// After a call that returned rc != hipSuccess and whose failure the caller handles with a fallback:
+// the thread's error state is consumed and logged.  A device fault is not a fallback case: thrown.
+inline void consume(hipError_t rc, const char *site) {
+  const hipError_t e = hipGetLastError();
+  const hipError_t r = rc != hipSuccess ? rc : e;
+  if (r == hipSuccess) return;
+  if (device_fault(r) || device_fault(e)) throw HipError{device_fault(r) ? r : e, site};
+  log_error(r, "handled", site, false);
+  if (e != hipSuccess && e != r) log_error(e, "pending", site, true);
+}
+
+// hipEventQuery's hipErrorNotReady is a status, not a failure: consumed silently; any other error
+// of the query is handled as consume() does.  Returns whether the event has completed.
+inline bool query_done(hipEvent_t ev, const char *site) {
+  const hipError_t rc = hipEventQuery(ev);
+  if (rc == hipSuccess) return true;
+  if (rc == hipErrorNotReady) {
+    if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();  // a status, not an error
+    return false;
+  }
+  consume(rc, site);
+  return true;  // a failed query: nothing better to wait for
+}
+
+// At an API entry: an error left in this thread's HIP error state was not raised by the library's
+// own calls (those are thrown or consumed where they happen) -- another library's, or an
+// asynchronous device fault.  Logged and printed; a device fault fails this call.
+inline void check_pending(const char *fn) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess || e == hipErrorNotReady) return;
+  log_error(e, "pending at entry", fn, true);
+  if (device_fault(e)) throw HipError{e, fn};
+}
 
 struct Event {
   hipEvent_t e = nullptr;
@@ -53,12 +142,21 @@ inline hipError_t record_event(hipStream_t s, EventPtr &out) {
   return rc;
 }
 
-// completed (or never recorded); a query error counts as completed -- nothing better to wait for
+// completed (or never recorded); a query error counts as completed -- nothing better to wait for.
+// Never throws (destructors prune readers): a device fault stays in the thread's error state for the
+// next API entry's check_pending, other query errors are consumed and logged.
 inline bool done(const EventPtr &ev) {
   if (!ev || !ev->e) return true;
   const hipError_t rc = hipEventQuery(ev->e);
-  if (rc == hipErrorNotReady) return false;
-  if (rc != hipSuccess) (void)hipGetLastError();
+  if (rc == hipSuccess) return true;
+  if (rc == hipErrorNotReady) {
+    if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();  // a status, not an error
+    return false;
+  }
+  if (!device_fault(rc)) {
+    (void)hipGetLastError();
+    log_error(rc, "handled", "hipEventQuery (buffer reader)", false);
+  }
   return true;
 }
 
@@ -187,7 +285,7 @@ inline void pool_clear(int device = -1) {
 inline hipError_t device_alloc(void **p, size_t bytes) {
   hipError_t rc = hipMalloc(p, bytes);
   if (rc == hipErrorOutOfMemory || rc == hipErrorMemoryAllocation) {
-    (void)hipGetLastError();
+    consume(rc, "hipMalloc (device full: pool and retired buffers reclaimed, retried)");
     int dev = 0;
     (void)hipGetDevice(&dev);
     pool_clear(dev);
@@ -300,7 +398,7 @@ struct LaunchRec {
     EventPtr ev;
     hipError_t rc = record_event(stream, ev);
     if (rc != hipSuccess) {  // cannot track: fall back to waiting here
-      (void)hipGetLastError();
+      consume(rc, "record_event (launch completion; waited for instead)");
       rc = hipStreamSynchronize(stream);
     }
     for (auto &b : reads)
@@ -339,7 +437,7 @@ struct Bounce {
     hipError_t rc = hipHostMalloc(reinterpret_cast<void **>(&pinned), PIECE * NB, hipHostMallocDefault);
     for (int i = 0; i < NB && rc == hipSuccess; ++i) rc = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
     if (rc != hipSuccess) {  // all or nothing
-      (void)hipGetLastError();
+      consume(rc, "Bounce::init (pinned bounce ring; the runtime's pageable copy instead)");
       for (hipEvent_t &e : ev)
         if (e) (void)hipEventDestroy(e), e = nullptr;
       if (pinned) (void)hipHostFree(pinned);

@@ -229,34 +229,6 @@ __device__ __forceinline__ float lerp_zrows(const f4a8 &r0, const f4a8 &r1, cons
   const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
   return lerp(c0, c1, az.w);
 }
-#if VR_LUT_ZPAIR == 2
-// VR_LUT_ZPAIR 2 (A/B, with VR_LUT_QUAD=1 on the host): the yz-quad copy, entries {v(i), v(i + pxy),
-// v(i + px), v(i + px + pxy)}; one lookup = the entries of x and x + 1 (32 contiguous bytes)
-__device__ __forceinline__ float lerp_quads(const f4a8 &e0, const f4a8 &e1, const AxF &ax, const AxF &ay,
-                                            const AxF &az) {
-  const float c00 = lerp(e0.x, e1.x, ax.w), c10 = lerp(e0.z, e1.z, ax.w);
-  const float c01 = lerp(e0.y, e1.y, ax.w), c11 = lerp(e0.w, e1.w, ax.w);
-  const float c0 = lerp(c00, c10, ay.w), c1 = lerp(c01, c11, ay.w);
-  return lerp(c0, c1, az.w);
-}
-__device__ __forceinline__ float fetch_small_z(const DevTex &t, const AxF &ax, const AxF &ay, const AxF &az) {
-  const uint32_t o = (uint32_t)fmaf(az.fl, t.fpxy4, fmaf(ay.fl, t.fpx4, fmaf(ax.fl, 4.f, t.fbase4)));
-  const char *b = reinterpret_cast<const char *>(t.zp) + 4u * o;
-  return lerp_quads(*reinterpret_cast<const f4a8 *>(b), *reinterpret_cast<const f4a8 *>(b + 16), ax, ay, az);
-}
-__device__ __forceinline__ void fetch_small2_z(const DevTex &t, const AxF &ax, const AxF &ay0, const AxF &az0,
-                                               const AxF &ay1, const AxF &az1, float &v0, float &v1) {
-  const float ox = fmaf(ax.fl, 4.f, t.fbase4);
-  const uint32_t o0 = (uint32_t)fmaf(az0.fl, t.fpxy4, fmaf(ay0.fl, t.fpx4, ox));
-  const uint32_t o1 = (uint32_t)fmaf(az1.fl, t.fpxy4, fmaf(ay1.fl, t.fpx4, ox));
-  const char *a = reinterpret_cast<const char *>(t.zp) + 4u * o0;
-  const char *b = reinterpret_cast<const char *>(t.zp) + 4u * o1;
-  const f4a8 a0 = *reinterpret_cast<const f4a8 *>(a), a1 = *reinterpret_cast<const f4a8 *>(a + 16);
-  const f4a8 b0 = *reinterpret_cast<const f4a8 *>(b), b1 = *reinterpret_cast<const f4a8 *>(b + 16);
-  v0 = lerp_quads(a0, a1, ax, ay0, az0);
-  v1 = lerp_quads(b0, b1, ax, ay1, az1);
-}
-#else
 __device__ __forceinline__ float fetch_small_z(const DevTex &t, const AxF &ax, const AxF &ay, const AxF &az) {
   const uint32_t o = (uint32_t)fmaf(az.fl, t.fpxy4, fmaf(ay.fl, t.fpx4, fmaf(ax.fl, 4.f, t.fbase4)));
   const uint32_t o2 = o + o, px8 = t.px * 8u;  // entries are 8 bytes
@@ -279,7 +251,6 @@ __device__ __forceinline__ void fetch_small2_z(const DevTex &t, const AxF &ax, c
   v0 = lerp_zrows(a0, a1, ax, ay0, az0);
   v1 = lerp_zrows(b0, b1, ax, ay1, az1);
 }
-#endif
 __device__ __forceinline__ Ax to_ax(const AxF &a) { return Ax{(int)a.fl, a.w}; }
 
 // The LUT value of one light (0 if the illumination texture is unbound).
@@ -465,6 +436,37 @@ __device__ __forceinline__ float divpi(float x) {
 #ifndef VR_FAST_COS
 #define VR_FAST_COS 1  // 1: the fast variant's cosines as dot * rsq * rsq; 0: correctly rounded (ablation)
 #endif
+#ifndef VR_FAST_NX
+#define VR_FAST_NX 0  // 1: the fast variant's unit normal as the oracle's, -(g * (1 / sqrtf(g.g))), bit for bit
+#endif
+#ifndef VR_FAST_GX
+#define VR_FAST_GX 0  // 1: the fast variant's gamma cosines correctly rounded (the oracle's quotient)
+#endif
+#ifndef VR_RSQ_NR
+#define VR_RSQ_NR 0  // 1: one Newton step on every cosine's hardware rsq
+#endif
+// rsq of a cosine normalisation (VR_RSQ_NR: one Newton step y (1 + (1 - x y^2) / 2))
+__device__ __forceinline__ float rsq_c(float x) {
+  const float y = __builtin_amdgcn_rsqf(x);
+#if VR_RSQ_NR
+  const float r = fmaf(-(x * y), y, 1.f);
+  return fmaf(r * 0.5f, y, y);
+#else
+  return y;
+#endif
+}
+// RN(1 / RN(sqrt(x))), the oracle's 1.f / sqrtf(x), for x >= 0: the correctly rounded root and
+// the compiler's correctly rounded reciprocal sequence without its range fix-ups where every lane
+// of the wave has x = 0 or 2^-80 <= x <= 2^80 (the root then in [2^-40, 2^40], div_fast's identity
+// range); x = 0 gives +inf, as 1 / 0.  Other waves take the library operations.
+__device__ __forceinline__ float rcp_sqrt_cr(float x) {
+  const uint32_t u = __float_as_uint(x);
+  if (__builtin_expect(__all(u == 0u || u - 0x17800000u <= 0x50000000u), 1)) {
+    const float r = div_fast(1.f, sqrt_fast(x));
+    return u == 0u ? __builtin_inff() : r;
+  }
+  return 1.f / sqrtf(x);
+}
 extern "C" __device__ float __ocml_acospi_f32(float);
 __device__ __forceinline__ float acospi_q(float q) {
 #if VR_ABLATE & 2
@@ -612,7 +614,11 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #endif
   if constexpr (FAST) {
     // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
+#if VR_FAST_NX
+    const float ginv = rcp_sqrt_cr(dot3(g, g));
+#else
     const float ginv = __builtin_amdgcn_rsqf(dot3(g, g));
+#endif
     const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
     const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
     const float dli = dot3(li, n);
@@ -621,10 +627,17 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
 #if VR_FAST_NLEN
     const float rn = 1.f;
 #else
-    const float rn = __builtin_amdgcn_rsqf(dot3(n, n));
+    const float rn = rsq_c(dot3(n, n));
 #endif
-    const float rlip = __builtin_amdgcn_rsqf(dot3(lip, lip));
-    const float alpha_n = acospi_q(dot3(n, li) * (rn * __builtin_amdgcn_rsqf(dot3(li, li))));
+#if VR_FAST_GX
+    // gamma's cosine as the oracle's dot(lip, lop) / (|lip| |lop|) (gamma_q): `rlip` holds |lip|
+    const float rlip = sqrt_cr(dot3(lip, lip));
+#define VR_GAMMA_Q(lop) div_acos_arg(dot3(lip, lop), rlip * sqrt_cr(dot3(lop, lop)))
+#else
+    const float rlip = rsq_c(dot3(lip, lip));
+#define VR_GAMMA_Q(lop) (dot3(lip, lop) * (rlip * rsq_c(dot3(lop, lop))))
+#endif
+    const float alpha_n = acospi_q(dot3(n, li) * (rn * rsq_c(dot3(li, li))));
     const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
     int i = 0;
     if (TAME || (P.lut.p != nullptr && P.lut.small && !P.lut.one)) {
@@ -637,10 +650,10 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
         const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
         const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
         const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-        const float beta0 = acospi_q(dlo0 * (rn * __builtin_amdgcn_rsqf(dot3(lo0, lo0))));
-        const float gamma0 = acospi_q(dot3(lip, lop0) * (rlip * __builtin_amdgcn_rsqf(dot3(lop0, lop0))));
-        const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
-        const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
+        const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
+        const float gamma0 = acospi_q(VR_GAMMA_Q(lop0));
+        const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
+        const float gamma1 = acospi_q(VR_GAMMA_Q(lop1));
         float light0, light1;
 #if VR_ABLATE & 1  // diagnostic: the LUT fetch's cost removed (wrong image)
         light0 = beta0 + gamma0 + la.w;
@@ -670,10 +683,10 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
       const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
       const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-      const float beta0 = acospi_q(dlo0 * (rn * __builtin_amdgcn_rsqf(dot3(lo0, lo0))));
-      const float gamma0 = acospi_q(dot3(lip, lop0) * (rlip * __builtin_amdgcn_rsqf(dot3(lop0, lop0))));
-      const float beta1 = acospi_q(dlo1 * (rn * __builtin_amdgcn_rsqf(dot3(lo1, lo1))));
-      const float gamma1 = acospi_q(dot3(lip, lop1) * (rlip * __builtin_amdgcn_rsqf(dot3(lop1, lop1))));
+      const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
+      const float gamma0 = acospi_q(VR_GAMMA_Q(lop0));
+      const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
+      const float gamma1 = acospi_q(VR_GAMMA_Q(lop1));
       const float light0 = lut_light<true>(P.lut, la, beta0, gamma0);
       const float light1 = lut_light<true>(P.lut, la, beta1, gamma1);
       const float rl0 = refl * light0;
@@ -690,8 +703,8 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
       const float dlo = dot3(lo, n);
       const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-      const float beta = acospi_q(dlo * (rn * __builtin_amdgcn_rsqf(dot3(lo, lo))));
-      const float gamma = acospi_q(dot3(lip, lop) * (rlip * __builtin_amdgcn_rsqf(dot3(lop, lop))));
+      const float beta = acospi_q(dlo * (rn * rsq_c(dot3(lo, lo))));
+      const float gamma = acospi_q(VR_GAMMA_Q(lop));
       const float rl = refl * (TAME ? (VR_LUT_ZPAIR ? fetch_small_z(P.lut, la, axis_lut<true>(beta, P.lut.fny),
                                                                    axis_lut<true>(gamma, P.lut.fnz))
                                                     : fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
@@ -701,6 +714,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
       ig = fmaf(rl * L.cg, P.color[1], ig);
       ib = fmaf(rl * L.cb, P.color[2], ib);
     }
+#undef VR_GAMMA_Q
   } else {
     // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
     // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n below

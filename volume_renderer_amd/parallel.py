@@ -38,6 +38,37 @@ def gather_partitions(local, gathered, world: int, rank: int, group=None) -> Non
     dist.gather(local, list(gathered.chunk(world)) if rank == 0 else None, dst=0, group=group)
 
 
+def rank_report(kernel_ms: float, gather_ms: float, world: int, rank: int, device=None, group=None):
+    """Per-rank attribution of a multi-GPU frame (bench.py at N > 1): every rank's mean march-kernel
+    time (HIP events around its launch) and its gather + assembly time (from the end of its launch
+    to the end of the RCCL gather -- on rank 0 also the on-device assembly; it includes waiting for
+    the slowest rank's kernel), all-gathered; and how many ranks the collective saw (an all-reduce of
+    ones).  Returns the dict on rank 0, None elsewhere.  Backend-agnostic (RCCL on the GPU, gloo in
+    the CPU test)."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([float(kernel_ms), float(gather_ms)], dtype=torch.float64, device=device)
+    if world > 1:
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine, group=group)
+        one = torch.ones(1, dtype=torch.int64, device=device)
+        dist.all_reduce(one, group=group)
+        seen, backend = int(one.item()), str(dist.get_backend(group))
+    else:
+        allv, seen, backend = [mine], 1, "none"
+    if rank != 0:
+        return None
+    k = [round(float(v[0].item()), 3) for v in allv]
+    g = [round(float(v[1].item()), 3) for v in allv]
+    return {"ranks_seen": seen, "backend": backend,
+            "kernel_ms_per_rank": k, "kernel_ms_max": max(k), "kernel_ms_min": min(k),
+            "kernel_imbalance": round(max(k) / min(k), 4) if min(k) > 0 else None,
+            "gather_assembly_ms_per_rank": g, "gather_assembly_ms_rank0": g[0],
+            "what": "mean over the timed frames: march kernel (HIP events around each rank's launch); "
+                    "gather + assembly = end of the rank's launch to the end of the gather (rank 0: + "
+                    "the on-device assembly; includes waiting for the slowest rank)"}
+
+
 # ---- sort-last z-slabs (SURVEY.md 8f row 1, DESIGN.md s9) -----------------------------------------
 # Volumes larger than one GPU: rank r holds only the planes of z-slab r (vr_slab_planes) and
 # marches only the samples that slab owns (vr_render_slab).  A ray's samples are composited in ray
