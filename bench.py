@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--pipelined-streams", type=int, default=2,
                     help="extra pass (not `value`): the frames issued round-robin on this many HIP streams "
                          "(independent frames of a movie, example3.m); 1 or 0 skips it")
+    ap.add_argument("--chunk-stats-k", action="store_true",
+                    help="diagnostic (a VR_COUNT_K=1 build): also the chunk statistics of the production "
+                         "depth lanes (the default counted launch runs at K = 1)")
     ap.add_argument("--traffic-json", default=_latest_traffic_json(),
                     help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
@@ -153,6 +156,20 @@ def main():
     wave_stats = [int(v) for v in steps_t[5:7].tolist()]
     fail_hist = [int(v) for v in steps_t[8:40].tolist()]
     staged_by_s = [int(v) for v in steps_t[40:44].tolist()]
+    prod_stats = None
+    if args.chunk_stats_k:  # the same counted launch at the production K (vr_capi.hip VR_COUNT_PROD)
+        steps_t.zero_()
+        os.environ["VR_COUNT_PROD"] = "1"
+        try:
+            mex.render_device(h, ra, out_local.data_ptr(), part, steps_t.data_ptr(), sptr)
+            torch.cuda.synchronize(dev)
+        finally:
+            del os.environ["VR_COUNT_PROD"]
+        prod_stats = {"kernel": mex.last_march_kernel(),
+                      "chunks_staged_leaped_global": [int(v) for v in steps_t[2:5].tolist()],
+                      "wave_iterations_total_lit": [int(v) for v in steps_t[5:7].tolist()],
+                      "staged_chunks_by_S_32_16_8_4": [int(v) for v in steps_t[40:44].tolist()],
+                      "global_chunk_box_hist_256": [int(v) for v in steps_t[8:40].tolist()]}
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     # N > 1: the end of each frame's gather (+ assembly on rank 0), for the per-rank attribution
@@ -322,6 +339,8 @@ def main():
                                            "(independent movie frames overlap their tails); not `value`"}
         if ranks is not None:
             result["ranks"] = ranks
+        if prod_stats is not None:
+            result["chunk_stats_production_k"] = prod_stats
         if sim is not None:
             result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
                                              "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}

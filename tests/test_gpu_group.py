@@ -31,10 +31,15 @@ def _scene(r, v, lit=True):
     return r
 
 
-@pytest.mark.parametrize("devices,replicate", [("0,0", "0"), ("0,0,0", "1"), ("0,0,0,0,0,0,0,0", "1")])
+@pytest.mark.parametrize("devices,replicate,peer", [("0,0", "0", "1"), ("0,0,0", "1", "1"),
+                                                   ("0,0,0,0,0,0,0,0", "1", "1"), ("0,0,0", "1", "0")])
 @pytest.mark.parametrize("grad", ["compute", "lookup"])
-def test_group_render_equals_one_device(monkeypatch, counter_clock, devices, replicate, grad):
+def test_group_render_equals_one_device(monkeypatch, counter_clock, devices, replicate, peer, grad):
+    """peer "0" (VR_GROUP_PEER=0): the group's children treated as without a peer mapping, so the
+    volume replicas and the part gathers go through pinned host memory (the branch a node without
+    xGMI peer access takes)."""
     monkeypatch.setenv("VR_GROUP_REPLICATE", replicate)
+    monkeypatch.setenv("VR_GROUP_PEER", peer)
     data = [O.shell_volume(48), np.asfortranarray(O.shell_volume(48)[::-1] * np.float32(0.7))]
 
     def frames(group):
@@ -128,13 +133,15 @@ def _ex3_channels(monkeypatch, devices, n=48, res=(90, 130)):
     return chans
 
 
-@pytest.mark.parametrize("devices", ["0,0", "0,0,0,0"])
-def test_group_fused_stereo_and_channels_equal_one_device(monkeypatch, counter_clock, devices):
+@pytest.mark.parametrize("devices,peer", [("0,0", "1"), ("0,0,0,0", "1"), ("0,0,0", "0")])
+def test_group_fused_stereo_and_channels_equal_one_device(monkeypatch, counter_clock, devices, peer):
     """The fused commands on group handles: a stereo pair (vr_render_stereo) and a C4-style
     two-channel stereo frame (vr_render_channels) rendered on a repeated-device group -- every device
     its column part of every view, parts gathered and assembled per view -- equal one device bit for
-    bit, over two frames (the second after a data change of one channel)."""
+    bit, over two frames (the second after a data change of one channel).  peer "0": host-staged
+    replicas and part gathers (VR_GROUP_PEER=0)."""
     monkeypatch.setenv("VR_GROUP_REPLICATE", "1")
+    monkeypatch.setenv("VR_GROUP_PEER", peer)
     out = {}
     for name, devs in (("one", None), ("group", devices)):
         chans = _ex3_channels(monkeypatch, devs)

@@ -358,7 +358,7 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
     keys = ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT",
-            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN")
+            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS")
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
@@ -369,7 +369,8 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
                       ("k4_big", {"VR_DEPTH_LANES": "4", "VR_FORCE_BIG": "1"}),
                       ("nosched", {"VR_SCHED": "0"}), ("k2_sched", {"VR_DEPTH_LANES": "2", "VR_SCHED": "1"}),
                       ("k1_sched", {"VR_DEPTH_LANES": "1", "VR_SCHED": "1"}),
-                      ("xcd_run2", {"VR_XCD_RUN": "2"}), ("k4_xcd_run4", {"VR_DEPTH_LANES": "4", "VR_XCD_RUN": "4"})]:
+                      ("xcd_run2", {"VR_XCD_RUN": "2"}), ("k4_xcd_run4", {"VR_DEPTH_LANES": "4", "VR_XCD_RUN": "4"}),
+                      ("rot3", {"VR_BLOCK_ROT_ROWS": "3"}), ("k4_rot2", {"VR_DEPTH_LANES": "4", "VR_BLOCK_ROT_ROWS": "2"})]:
         for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():

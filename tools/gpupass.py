@@ -9,13 +9,15 @@ Steps ('|' separates variants, ',' environment assignments inside a variant):
   tests[:K_EXPR]                 pytest -m gpu (optionally -k K_EXPR)            -> tests.log
   ab:ROUNDS:NAME=ENV,..|NAME=..  interleaved same-box bench.py A/B (serial frames, 20 steps); a
                                  variant's ENV may hold VR_LIB_PATH=build_ab/libvrhip_X.so; extra
-                                 bench args from $BENCH_ARGS                       -> ab.jsonl, ab.txt
+                                 bench args from the last args: step    -> abN.jsonl, abN.txt (N-th ab)
+  args:BENCH_ARGS                bench.py arguments of the following ab steps (e.g. --width 1024
+                                 --height 768; '-' for none)
   abl:SCENES:NAME=LIB[;ENV,..]|..  tools/shade_ablation.py parity of shading variants on the scenes
                                  (c2, metric, c4_main, c4_struct)                  -> ablation.json
   bench[:ARGS]                   the bench line (CPU baseline included unless ARGS say otherwise)
                                                                                    -> bench.json
-  kt[:ARGS]                      rocprofv3 --kernel-trace --stats of bench.py      -> kt/
-  pmc[:ARGS]                     tools/pmc.sh counter passes (one group per pass)  -> pmc/
+  kt[:ARGS]                      rocprofv3 --kernel-trace --stats of bench.py      -> ktN/ (N-th kt)
+  pmc[:ARGS]                     tools/pmc.sh counter passes (one group per pass)  -> pmcN/ (N-th pmc)
   py:SCRIPT[ ARGS]               any python script of the tree (e.g. tools/tail_profile.py ...)
 """
 import json
@@ -49,19 +51,19 @@ def parse_env(spec):
     return env
 
 
-def step_ab(out, rest):
+def step_ab(out, rest, idx, bench_args):
     rounds, variants = rest.split(":", 1)
     specs = []
     for v in variants.split("|"):
         name, _, envs = v.partition("=")
         specs.append((name, parse_env(envs)))
-    jl = os.path.join(out, "ab.jsonl")
-    extra = shlex.split(os.environ.get("BENCH_ARGS", ""))
+    jl = os.path.join(out, f"ab{idx}.jsonl")
+    extra = shlex.split(bench_args)
     for r in range(int(rounds)):
         for name, env in specs:
             e = dict(os.environ)
             e.update(env)
-            res = os.path.join(out, f"ab_{name}_{r}.json")
+            res = os.path.join(out, f"ab{idx}_{name}_{r}.json")
             cmd = [PY, "bench.py", "--steps", "20", "--warmup", "4", "--no-cpu-baseline", "--pipelined-streams", "0"]
             with open(res, "wb") as fh:
                 rc = subprocess.run(["timeout", "-k", "10", "300"] + cmd + extra, cwd=ROOT, stdout=fh,
@@ -71,7 +73,7 @@ def step_ab(out, rest):
                 return rc
             line = json.loads(open(res).read().strip().splitlines()[-1])
             with open(jl, "a") as fh:
-                fh.write(json.dumps({"ab": name, "round": r, "line": line}) + "\n")
+                fh.write(json.dumps({"ab": name, "round": r, "args": bench_args, "line": line}) + "\n")
             rf = line.get("roofline", {})
             print(f"  ab {name:10s} round {r}: frame {line['ms_per_step']:.3f} ms, kernel {rf.get('kernel_ms')} ms, "
                   f"sha {str(line.get('image_sha256', ''))[:12]}", flush=True)
@@ -79,7 +81,8 @@ def step_ab(out, rest):
     for l in open(jl):
         d = json.loads(l)
         summary.setdefault(d["ab"], []).append(d["line"]["roofline"].get("kernel_ms"))
-    with open(os.path.join(out, "ab.txt"), "w") as fh:
+    with open(os.path.join(out, f"ab{idx}.txt"), "w") as fh:
+        fh.write(f"bench args: {bench_args or '(default)'}\n")
         for k, v in summary.items():
             fh.write(f"{k} {v} min {min(v)}\n")
     return 0
@@ -89,6 +92,7 @@ def main():
     run_name, steps = sys.argv[1], sys.argv[2:]
     out = os.path.join(ROOT, "gpurun_out", run_name)
     os.makedirs(out, exist_ok=True)
+    n_ab, n_kt, n_pmc, bench_args = 0, 0, 0, ""
     for st in steps:
         kind, _, rest = st.partition(":")
         print(f"step {kind}: {rest[:120]}", flush=True)
@@ -97,7 +101,11 @@ def main():
                    "--timeout-method", "thread"] + (["-k", rest] if rest else [])
             rc = run(cmd, os.path.join(out, "tests.log"), 900)
         elif kind == "ab":
-            rc = step_ab(out, rest)
+            n_ab += 1
+            rc = step_ab(out, rest, n_ab, bench_args)
+        elif kind == "args":
+            bench_args = "" if rest == "-" else rest
+            rc = 0
         elif kind == "abl":
             scenes, variants = rest.split(":", 1)
             args = [v.replace(";", ":", 1) for v in variants.split("|")]
@@ -113,11 +121,14 @@ def main():
             args = shlex.split(rest) or ["--steps", "10", "--warmup", "2", "--no-cpu-baseline", "--pipelined-streams",
                                          "0"]
             e = dict(os.environ, TMPDIR="/tmp")
-            rc = run(["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(out, "kt"), "-o", "kt",
-                      "--output-format", "csv", "--", PY, "bench.py"] + args, os.path.join(out, "kt.log"), 400, env=e)
+            n_kt += 1
+            rc = run(["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(out, f"kt{n_kt}"), "-o", "kt",
+                      "--output-format", "csv", "--", PY, "bench.py"] + args, os.path.join(out, f"kt{n_kt}.log"), 400,
+                     env=e)
         elif kind == "pmc":
-            rc = run(["bash", "tools/pmc.sh", os.path.join(out, "pmc")] + shlex.split(rest),
-                     os.path.join(out, "pmc.log"), 1000)
+            n_pmc += 1
+            rc = run(["bash", "tools/pmc.sh", os.path.join(out, f"pmc{n_pmc}")] + shlex.split(rest),
+                     os.path.join(out, f"pmc{n_pmc}.log"), 1000)
         elif kind == "py":
             rc = run([PY, "-u"] + shlex.split(rest), os.path.join(out, "py.log"), 900)
         else:

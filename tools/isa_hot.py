@@ -48,3 +48,8 @@ trans = sum(n for k, n in c.items() if k.startswith(("v_rsq", "v_sqrt", "v_exp",
 print(f"loop BB{hdr}: {len(loop)} blocks, common path {len(hot)}: instructions {sum(c.values())}, VALU {valu} "
       f"(slow class {slow}, transcendental {trans}), readlane {c['v_readlane_b32']}, s_nop {c['s_nop']}, "
       f"scratch {c['scratch_load_dword'] + c['scratch_load_dwordx2']}, LDS {sum(n for k, n in c.items() if k.startswith('ds_'))}")
+if len(sys.argv) > 2 and sys.argv[2] == "--dump":
+    for b in hot:
+        print(b["name"], b["hdr"][:80])
+        for x in b["ins"]:
+            print("   ", x)

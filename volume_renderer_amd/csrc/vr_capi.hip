@@ -265,6 +265,9 @@ struct vr_context {
   vr_context *parent = nullptr;
   hipStream_t gstream = nullptr;  // child: its device's stream (replica copies, render, gather)
   hipEvent_t gdone = nullptr;     // child: its part has landed on the primary
+  // child: whether copies between it and the primary go over a peer mapping (xGMI); without one
+  // (hipDeviceCanAccessPeer 0, or VR_GROUP_PEER=0) they are staged through pinned host memory
+  bool peer = true;
   float *d_part = nullptr;        // child: its part image; primary: all parts
   size_t d_part_bytes = 0;
   // the last launch's kernel time on this context's device (events around the march launch of
@@ -1128,6 +1131,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
   P.xcd_run = VR_XCD_RUN;
   if (const char *ev = std::getenv("VR_XCD_RUN")) P.xcd_run = std::max(0, std::atoi(ev));  // A/B switch
+  P.block_rot = 0;  // set at the launch (block rows of the launch's depth lanes)
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
   if (d_out2) {
     P.views = 2;
@@ -1188,7 +1192,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   bind_reads(L);
   stage_frame(L, P, g_tex.lights);
   if (march) {
-    const int K = P.steps ? 1 : exact_lanes(depth_lanes(P), P.fast_shade);  // the counter variant: K = 1
+    // the counter variant: K = 1 (VR_COUNT_PROD=1 with a VR_COUNT_K=1 build: the production K's chunk
+    // statistics; its sample sums are then 0)
+    const int K = (P.steps && !env_flag("VR_COUNT_PROD")) ? 1 : exact_lanes(depth_lanes(P), P.fast_shade);
     set_chunk_halo(F, K);
     typedef hipError_t (*launch_fn)(const vr::RenderParams &, int, bool, bool, bool, hipStream_t);
     typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
@@ -1214,6 +1220,18 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_start), (size_t)P.sched_blocks * 4);
       if (e == hipSuccess) P.wg_start = d_start;
       else vr_host::consume(e, "hipMalloc (VR_SCHED_DUMP start ticks; not recorded)");
+    }
+    // VR_BLOCK_ROT_ROWS=r (A/B): the unscheduled launch starts at block row r of the row-major order
+    // and wraps (the light top rows then fill the ramp-down of the heavy middle band)
+    if (const char *ev = std::getenv("VR_BLOCK_ROT_ROWS")) {
+      const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
+      const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
+      typedef uint32_t (*bfn)(const vr::RenderParams &);
+      static const bfn bf[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
+                                VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
+      const uint32_t nb = bf[ki](P) * (P.views > 1 ? 2u : 1u);
+      const uint64_t rot = (uint64_t)std::max(0, std::atoi(ev)) * nbx;
+      P.block_rot = nb ? (uint32_t)(rot % nb) : 0u;
     }
     time_mark(h, 0, stream);
     {
@@ -1350,9 +1368,35 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
 
 // ---- multi-device group (vr_new_multi) ----------------------------------------------------------
 
+// A device-to-device copy through pinned host memory, for device pairs without a peer mapping: the
+// D2H is issued on `ss` (a stream of sdev) -- synchronously when ss is null --, the H2D on `ds` (a
+// stream of ddev) after it; the pinned buffer is released when the H2D has completed.  Returns the
+// completion event of the H2D.
+vr_host::EventPtr staged_copy(void *dst, int ddev, hipStream_t ds, const void *src, int sdev, hipStream_t ss,
+                              size_t bytes) {
+  void *pin = nullptr;
+  VR_HIP(hipHostMalloc(&pin, bytes, hipHostMallocDefault));
+  vr_host::EventPtr e1, e2;
+  {
+    DeviceGuard g(sdev);
+    if (ss) {
+      VR_HIP(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, ss));
+      VR_HIP(vr_host::record_event(ss, e1));
+    } else {
+      VR_HIP(hipMemcpy(pin, src, bytes, hipMemcpyDeviceToHost));
+    }
+  }
+  DeviceGuard g(ddev);
+  if (e1) VR_HIP(hipStreamWaitEvent(ds, e1->e, 0));
+  VR_HIP(hipMemcpyAsync(dst, pin, bytes, hipMemcpyHostToDevice, ds));
+  VR_HIP(vr_host::record_event(ds, e2));
+  vr_host::free_when_done(pin, ddev, vr_host::readers_of(e2), true);
+  return e2;
+}
+
 // The copy of buffer b on device `dev`, refreshed when b was re-uploaded since (peer copy over xGMI on
 // the device's group stream; a replica a launch still reads is replaced, not overwritten).
-BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
+BufPtr replicate(const BufPtr &b, int dev, hipStream_t s, bool peer = true) {
   if (!b) return b;
   if (b->device == dev && !env_flag("VR_GROUP_REPLICATE")) return b;  // test switch: copy on one device too
   BufPtr &r = b->replicas[dev];
@@ -1367,10 +1411,15 @@ BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
     }
   }
   if (b->bytes) {
-    VR_HIP(hipMemcpyPeerAsync(r->ptr, dev, b->ptr, b->device, b->bytes, s));
-    // the copy reads b and writes r: neither is rewritten, pooled or freed before it completes
     vr_host::EventPtr ev;
-    VR_HIP(vr_host::record_event(s, ev));
+    if (peer) {
+      VR_HIP(hipMemcpyPeerAsync(r->ptr, dev, b->ptr, b->device, b->bytes, s));
+      VR_HIP(vr_host::record_event(s, ev));
+    } else {  // no peer mapping: through pinned host memory (b is resident: its D2H runs now)
+      if (b->ready) vr_host::wait(b->ready);
+      ev = staged_copy(r->ptr, dev, s, b->ptr, b->device, nullptr, b->bytes);
+    }
+    // the copy reads b and writes r: neither is rewritten, pooled or freed before it completes
     b->readers.add(ev);
     r->readers.add(ev);
     r->ready = ev;
@@ -1386,15 +1435,22 @@ BufPtr replicate(const BufPtr &b, int dev, hipStream_t s) {
   return r;
 }
 
-void enable_peer(int a, int b) {
-  if (a == b) return;
+// Whether device a may map b's memory (the mapping enabled); false: copies between them are staged
+// through pinned host memory (staged_copy).
+bool enable_peer(int a, int b) {
+  if (a == b) return true;
   int ok = 0;
-  if (hipDeviceCanAccessPeer(&ok, a, b) == hipSuccess && ok) {
-    DeviceGuard dg(a);
-    const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-    // already enabled / unsupported: peer copies still work (through the host if need be)
-    if (e != hipSuccess) vr_host::consume(e, "hipDeviceEnablePeerAccess (group peer mapping)");
+  const hipError_t q = hipDeviceCanAccessPeer(&ok, a, b);
+  if (q != hipSuccess) {
+    vr_host::consume(q, "hipDeviceCanAccessPeer (group peer mapping; copies staged through the host)");
+    return false;
   }
+  if (!ok) return false;
+  DeviceGuard dg(a);
+  const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+  if (e == hipSuccess) return true;
+  vr_host::consume(e, "hipDeviceEnablePeerAccess (group peer mapping)");
+  return e == hipErrorPeerAccessAlreadyEnabled;
 }
 
 // After a sync of the primary: the children record the same volumes, and the bound volumes are
@@ -1405,7 +1461,7 @@ void group_sync(vr_context *h) {
     for (int t = 0; t < T_COUNT; ++t) c->vol[t] = h->vol[t];
     c->time_last_mem_sync = h->time_last_mem_sync;
     for (int t = 0; t < T_COUNT; ++t)
-      if (t != T_LIGHT && g_tex.bind[t]) (void)replicate(g_tex.bind[t], c->device, c->gstream);
+      if (t != T_LIGHT && g_tex.bind[t]) (void)replicate(g_tex.bind[t], c->device, c->gstream, c->peer);
   }
 }
 
@@ -1439,7 +1495,7 @@ void ensure_part_buffers(vr_context *h, int n, size_t part_floats, int nviews) {
 void bind_replicas(vr_context *h, vr_context *c, const BufPtr (&saved)[T_COUNT]) {
   for (int t = 0; t < T_COUNT; ++t) c->vol[t] = h->vol[t];
   for (int t = 0; t < T_COUNT; ++t)
-    g_tex.bind[t] = t == T_LIGHT ? c->buf[T_LIGHT] : replicate(saved[t], c->device, c->gstream);
+    g_tex.bind[t] = t == T_LIGHT ? c->buf[T_LIGHT] : replicate(saved[t], c->device, c->gstream, c->peer);
 }
 
 // Gather every child's parts (nviews images each) into the primary's part buffer over xGMI and
@@ -1452,10 +1508,17 @@ void group_gather_assemble(vr_context *h, int nviews, size_t part_floats, int64_
     DeviceGuard dg(c->device);
     // the previous frame's assembly has read these slots of the primary's part buffer
     VR_HIP(hipStreamWaitEvent(c->gstream, h->gdone, 0));
-    for (int v = 0; v < nviews; ++v)
-      VR_HIP(hipMemcpyPeerAsync(h->d_part + ((size_t)v * n + k) * part_floats, h->device,
-                                c->d_part + (size_t)v * part_floats, c->device, part_floats * sizeof(float),
-                                c->gstream));
+    if (c->peer) {
+      for (int v = 0; v < nviews; ++v)
+        VR_HIP(hipMemcpyPeerAsync(h->d_part + ((size_t)v * n + k) * part_floats, h->device,
+                                  c->d_part + (size_t)v * part_floats, c->device, part_floats * sizeof(float),
+                                  c->gstream));
+    } else {  // no peer mapping: D2H on the child's stream, H2D on the primary's (after the previous
+              // frame's assembly, which read these slots, in that stream's order)
+      for (int v = 0; v < nviews; ++v)
+        (void)staged_copy(h->d_part + ((size_t)v * n + k) * part_floats, h->device, stream,
+                          c->d_part + (size_t)v * part_floats, c->device, c->gstream, part_floats * sizeof(float));
+    }
     VR_HIP(hipEventRecord(c->gdone, c->gstream));
   }
   for (vr_context *c : h->children) VR_HIP(hipStreamWaitEvent(stream, c->gdone, 0));
@@ -1655,12 +1718,14 @@ int vr_new_multi(const int32_t *devices, int32_t n, vr_context **out) {
   vr_context *h = new vr_context();
   h->device = devices[0];
   VR_HIP(hipEventCreateWithFlags(&h->gdone, hipEventDisableTiming));
+  // VR_GROUP_PEER=0 (test switch): every child as if without a peer mapping (host-staged copies)
+  const bool no_peer = env_flag_off("VR_GROUP_PEER");
   for (int i = 1; i < n; ++i) {
-    enable_peer(devices[0], devices[i]);
-    enable_peer(devices[i], devices[0]);
+    const bool peer = enable_peer(devices[0], devices[i]) && enable_peer(devices[i], devices[0]) && !no_peer;
     DeviceGuard dk(devices[i]);
     vr_context *c = new vr_context();
     c->device = devices[i];
+    c->peer = peer;
     c->parent = h;
     h->children.push_back(c);
     VR_HIP(take_stream(c->device, &c->gstream));

@@ -42,6 +42,12 @@
 #ifndef VR_WHOLE_SPLIT
 #define VR_WHOLE_SPLIT 1  // K > 1: the sample loop compiled twice, for whole chunks and the others
 #endif
+#ifndef VR_COUNT_K
+// 1 (diagnostic builds): the counter variant is also built for K > 1 -- the chunk statistics of the
+// production depth lanes (staged / leaped / global chunks, S histogram, wave iterations); its sample
+// sums stay the K = 1 variant's (host: VR_COUNT_PROD=1 routes a counted launch here)
+#define VR_COUNT_K 0
+#endif
 #if VR_CHECK_WHOLE
 static __device__ unsigned long long vr_whole_violations;  // (diagnostic build) samples the whole-box rule misses
 #endif
@@ -236,7 +242,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   shaded = MODE != 0 && !skip;
   if (MODE != 0 && !skip) {
     f3 g;
-    if (MODE == 1 && (VR_ABLATE & 4)) {
+    if ((MODE == 1 && (VR_ABLATE & 4)) || (MODE == 2 && (VR_ABLATE & 32))) {  // diagnostics: no gradient fetch
       g = mk(ps.x, ps.y, em_s);
     } else if (HALF_TAPS && (HALF_ONLY || P.tap_half) &&
                (full || __all(staged && (unsigned)(lx + (sx.hi ? 1 : 0) - 1) < (unsigned)(B.ex - 2) &&
@@ -411,7 +417,7 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
                                       uint32_t kk = 0) {
-  static_assert(!COUNT || K == 1, "the counter variant is built for K = 1 only");
+  static_assert(!COUNT || K == 1 || VR_COUNT_K, "the counter variant is built for K = 1 only (VR_COUNT_K: all K)");
   static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
   const float sbz = P.bmin[2], ssz = P.bscale[2];
   // slab mode: the ray has left the slab in its direction of travel (normalized z of its sample)
@@ -547,10 +553,14 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           if (ex && beyond(zn)) ex = false;
           take = ex && zn >= P.slab_z0 && zn < P.slab_z1;
         }
+        bool shaded = false;
         if (take) {
-          bool shaded;
           sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, WC || (!VR_WHOLE_SPLIT && whole), R.pos,
                                                          R.o, r, gg, b, alpha, shaded);
+        }
+        if (COUNT) {
+          ++C.iter;
+          C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
         }
         composite_group<K, 0, VR_ZERO_FILL && !NANCHK && !SLAB>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
         if (SLAB && !inside) {
@@ -646,7 +656,11 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   float *L = lds[wave];
   constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
+  uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
+  if (!SCHED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
+    wgo += P.block_rot;
+    if (wgo >= gridDim.x) wgo -= gridDim.x;
+  }
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
   if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
   // fused stereo: the second view's workgroups follow the first's (same rays, other eye)
@@ -703,7 +717,8 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     }
   }
   if (COUNT) {
-    unsigned long long s = (unsigned long long)R.nsteps, l = (unsigned long long)R.nlit;
+    // (K > 1: the lanes' sample indices are not the ray's sample count -- the sums are the K = 1 variant's)
+    unsigned long long s = K == 1 ? (unsigned long long)R.nsteps : 0ull, l = K == 1 ? (unsigned long long)R.nlit : 0ull;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       s += __shfl_xor(s, off, 64);
@@ -990,6 +1005,9 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   if (K == 1 && P.steps) {
     if (big) VR_LAUNCH(1, true, true, 0, 0);
     else VR_LAUNCH(1, true, false, 0, 0);
+  } else if (VR_COUNT_K && P.steps) {  // diagnostic build: chunk statistics at the production K
+    if (big) VR_LAUNCH(K, VR_COUNT_K != 0, true, 0, 0);
+    else VR_LAUNCH(K, VR_COUNT_K != 0, false, 0, 0);
   } else if (!VR_MARCH_FAST && sched) {  // the exact variant is built without the scheduled kernels
     return hipErrorInvalidValue;
   } else if (K > 1 && sched && P.sched_full == 1) {  // a full frame, durations measured
@@ -1033,7 +1051,7 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
                                               hipStream_t s) {
   using TS = TileShape<VR_MARCH_K>;
   if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
-  if (VR_MARCH_K != 1 && P.steps) return hipErrorInvalidValue;
+  if (VR_MARCH_K != 1 && !VR_COUNT_K && P.steps) return hipErrorInvalidValue;
   const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);

@@ -366,7 +366,7 @@ __device__ __forceinline__ bool ray_setup(const RenderParams &P, int x, int y, f
 // the LUT lookup, accumulated as ((refl*light)*lc)*color + result.  `refl` is Fr * R(p).
 #ifndef VR_ABLATE
 #define VR_ABLATE 0  // diagnostic builds only (tools/ablate_build.sh): 1 LUT, 2 angles, 4 taps, 8 exp,
-                     // 16 no staged-box check
+                     // 16 no staged-box check, 32 no lookup-gradient fetch
 #endif
 
 // a / b for the arguments of the angle acosf calls, bit-identical to IEEE a / b wherever it can
@@ -393,6 +393,13 @@ __device__ __forceinline__ float div_fast(float a, float b) {
   const float q0 = a * y1;
   const float q1 = fmaf(fmaf(-b, q0, a), y1, q0);
   return fmaf(fmaf(-b, q1, a), y1, q1);
+}
+// a / b with one residual correction on the hardware reciprocal (no Newton step on it): not always
+// correctly rounded (tools/microbench/cosine_check.hip counts how often it is not).
+__device__ __forceinline__ float div_short(float a, float b) {
+  const float y = __builtin_amdgcn_rcpf(b);
+  const float q0 = a * y;
+  return fmaf(fmaf(-b, q0, a), y, q0);
 }
 // div_acos_arg over a group with one wave-wide guard (see div_acos_arg for the exactness argument).
 template <int N>
@@ -441,6 +448,24 @@ __device__ __forceinline__ float divpi(float x) {
 #endif
 #ifndef VR_FAST_GX
 #define VR_FAST_GX 0  // 1: the fast variant's gamma cosines correctly rounded (the oracle's quotient)
+#endif
+#ifndef VR_FAST_NXQ
+#define VR_FAST_NXQ 0  // 1: the fast normal as -(g * v_rcp(v_sqrt(g.g))) (the oracle's op sequence, hardware ops)
+#endif
+#ifndef VR_FAST_GXQ
+#define VR_FAST_GXQ 0  // 1: gamma's cosine as dot / (v_sqrt(lip.lip) v_sqrt(lop.lop)), one-correction quotient
+#endif
+#ifndef VR_FAST_HYBQ
+#define VR_FAST_HYBQ 0  // 1: gamma's cosine correctly rounded (the oracle's) only in waves with |cos| > VR_HYB_TG
+#endif
+#ifndef VR_FAST_HYBRID
+#define VR_FAST_HYBRID 0  // 1: rsq shading, and XN + XG shading where gamma is ill-conditioned (shade_fast)
+#endif
+#ifndef VR_HYB_TA
+#define VR_HYB_TA 0.01f  // hybrid: |lip|^2 < TA |li|^2 (view within asin(0.1) of the normal), same for lights
+#endif
+#ifndef VR_HYB_TG
+#define VR_HYB_TG 0.995f  // hybrid: |cos gamma| > TG
 #endif
 #ifndef VR_RSQ_NR
 #define VR_RSQ_NR 0  // 1: one Newton step on every cosine's hardware rsq
@@ -571,6 +596,132 @@ __device__ __forceinline__ float voxel0(const float *p) {
   return ((cptr)p)[0];
 }
 
+// The fast variant's shading (shade_lights FAST).  XN: the unit normal bit for bit as the oracle's
+// (the correctly rounded 1 / sqrtf); XG: gamma's cosine as the oracle's correctly rounded quotient.
+// NEED: set `need` where the sample's gamma is ill-conditioned -- the view or a light direction
+// within asin(sqrt(VR_HYB_TA)) of the normal (its projection onto the tangent plane cancels, so the
+// normal's last bits decide its direction) or a gamma cosine beyond +-VR_HYB_TG (acos amplifies the
+// cosine's rounding there) -- where the hybrid shading (VR_FAST_HYBRID) takes XN + XG.
+template <bool TAME, bool XN, bool XG, bool NEED>
+__device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
+                                          const float refl, float &ir, float &ig, float &ib, bool &need) {
+  // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
+  float ginv;
+  if constexpr (XN) ginv = rcp_sqrt_cr(dot3(g, g));  // the oracle's 1 / sqrtf(g.g), bit for bit
+  else if (VR_FAST_NXQ) ginv = __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(dot3(g, g)));
+  else ginv = __builtin_amdgcn_rsqf(dot3(g, g));
+  const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
+  const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
+  const float dli = dot3(li, n);
+  const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
+  // |n| is 1 to within the rsq's ulp: its length is not divided out again (VR_FAST_NLEN 0 does)
+#if VR_FAST_NLEN
+  const float rn = 1.f;
+#else
+  const float rn = rsq_c(dot3(n, n));
+#endif
+  // XG: gamma's cosine as the oracle's dot(lip, lop) / (|lip| |lop|): `rlip` then holds |lip|
+  const float lip2 = dot3(lip, lip), li2 = dot3(li, li);
+  const float rlip = XG ? sqrt_cr(lip2) : (VR_FAST_GXQ ? __builtin_amdgcn_sqrtf(lip2) : rsq_c(lip2));
+  // the cosine of gamma for light vector lo (its projection lop); NEED: the sample is in a region
+  // where gamma is ill-conditioned (see shade_lights)
+  auto gamma_q = [&](const f3 &lo, const f3 &lop) {
+    const float lop2 = dot3(lop, lop);
+    float q;
+    if constexpr (XG) q = div_acos_arg(dot3(lip, lop), rlip * sqrt_cr(lop2));
+    else if (VR_FAST_GXQ) q = div_short(dot3(lip, lop), rlip * __builtin_amdgcn_sqrtf(lop2));
+    else q = dot3(lip, lop) * (rlip * rsq_c(lop2));
+    if constexpr (NEED) need = need || fabsf(q) > VR_HYB_TG || lop2 < VR_HYB_TA * dot3(lo, lo);
+    if constexpr (VR_FAST_HYBQ && !XG && !NEED) {
+      // near |cos| = 1 acos amplifies the cosine's rounding: there the oracle's quotient
+      const bool nd = fabsf(q) > VR_HYB_TG;
+      if (__builtin_expect(__any(nd), 0)) {
+        const float qx = div_acos_arg(dot3(lip, lop), sqrt_cr(lip2) * sqrt_cr(lop2));
+        if (nd) q = qx;
+      }
+    }
+    return q;
+  };
+  if constexpr (NEED) need = lip2 < VR_HYB_TA * li2;
+  const float alpha_n = acospi_q(dot3(n, li) * (rn * rsq_c(li2)));
+  const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
+  int i = 0;
+  if (TAME || (P.lut.p != nullptr && P.lut.small && !P.lut.one)) {
+    // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
+    // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
+    for (; i + 1 < P.num_lights; i += 2) {
+      const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
+      const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
+      const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
+      const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
+      const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
+      const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
+      const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
+      const float gamma0 = acospi_q(gamma_q(lo0, lop0));
+      const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
+      const float gamma1 = acospi_q(gamma_q(lo1, lop1));
+      float light0, light1;
+#if VR_ABLATE & 1  // diagnostic: the LUT fetch's cost removed (wrong image)
+      light0 = beta0 + gamma0 + la.w;
+      light1 = beta1 + gamma1 + la.w;
+#else
+      if (TAME && VR_LUT_ZPAIR)  // the host binds a tame launch's LUT with its z-paired copy
+        fetch_small2_z(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
+                       axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
+      else
+        fetch_small2(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
+                     axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
+#endif
+      const float rl0 = refl * light0;
+      ir = fmaf(rl0 * L0.cr, P.color[0], ir);
+      ig = fmaf(rl0 * L0.cg, P.color[1], ig);
+      ib = fmaf(rl0 * L0.cb, P.color[2], ib);
+      const float rl1 = refl * light1;
+      ir = fmaf(rl1 * L1.cr, P.color[0], ir);
+      ig = fmaf(rl1 * L1.cg, P.color[1], ig);
+      ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+    }
+  }
+  if constexpr (!TAME) for (; i + 1 < P.num_lights; i += 2) {
+    const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
+    const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
+    const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
+    const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
+    const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
+    const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
+    const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
+    const float gamma0 = acospi_q(gamma_q(lo0, lop0));
+    const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
+    const float gamma1 = acospi_q(gamma_q(lo1, lop1));
+    const float light0 = lut_light<true>(P.lut, la, beta0, gamma0);
+    const float light1 = lut_light<true>(P.lut, la, beta1, gamma1);
+    const float rl0 = refl * light0;
+    ir = fmaf(rl0 * L0.cr, P.color[0], ir);
+    ig = fmaf(rl0 * L0.cg, P.color[1], ig);
+    ib = fmaf(rl0 * L0.cb, P.color[2], ib);
+    const float rl1 = refl * light1;
+    ir = fmaf(rl1 * L1.cr, P.color[0], ir);
+    ig = fmaf(rl1 * L1.cg, P.color[1], ig);
+    ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+  }
+  if (i < P.num_lights) {
+    const DevLight L = light_at(P, i);
+    const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
+    const float dlo = dot3(lo, n);
+    const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
+    const float beta = acospi_q(dlo * (rn * rsq_c(dot3(lo, lo))));
+    const float gamma = acospi_q(gamma_q(lo, lop));
+    const float rl = refl * (TAME ? (VR_LUT_ZPAIR ? fetch_small_z(P.lut, la, axis_lut<true>(beta, P.lut.fny),
+                                                                 axis_lut<true>(gamma, P.lut.fnz))
+                                                  : fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
+                                                                axis_lut<true>(gamma, P.lut.fnz)))
+                                  : lut_light<true>(P.lut, la, beta, gamma));
+    ir = fmaf(rl * L.cr, P.color[0], ir);
+    ig = fmaf(rl * L.cg, P.color[1], ig);
+    ib = fmaf(rl * L.cb, P.color[2], ib);
+  }
+}
+
 template <bool FAST, bool TAME = false>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib) {
@@ -613,108 +764,27 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
   } else
 #endif
   if constexpr (FAST) {
-    // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
-#if VR_FAST_NX
-    const float ginv = rcp_sqrt_cr(dot3(g, g));
-#else
-    const float ginv = __builtin_amdgcn_rsqf(dot3(g, g));
-#endif
-    const f3 n = mk(-(g.x * ginv), -(g.y * ginv), -(g.z * ginv));
-    const f3 li = mk(o.x - pos.x, o.y - pos.y, o.z - pos.z);
-    const float dli = dot3(li, n);
-    const f3 lip = mk(fmaf(-dli, n.x, li.x), fmaf(-dli, n.y, li.y), fmaf(-dli, n.z, li.z));
-    // |n| is 1 to within the rsq's ulp: its length is not divided out again (VR_FAST_NLEN 0 does)
-#if VR_FAST_NLEN
-    const float rn = 1.f;
-#else
-    const float rn = rsq_c(dot3(n, n));
-#endif
-#if VR_FAST_GX
-    // gamma's cosine as the oracle's dot(lip, lop) / (|lip| |lop|) (gamma_q): `rlip` holds |lip|
-    const float rlip = sqrt_cr(dot3(lip, lip));
-#define VR_GAMMA_Q(lop) div_acos_arg(dot3(lip, lop), rlip * sqrt_cr(dot3(lop, lop)))
-#else
-    const float rlip = rsq_c(dot3(lip, lip));
-#define VR_GAMMA_Q(lop) (dot3(lip, lop) * (rlip * rsq_c(dot3(lop, lop))))
-#endif
-    const float alpha_n = acospi_q(dot3(n, li) * (rn * rsq_c(dot3(li, li))));
-    const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
-    int i = 0;
-    if (TAME || (P.lut.p != nullptr && P.lut.small && !P.lut.one)) {
-      // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
-      // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
-      for (; i + 1 < P.num_lights; i += 2) {
-        const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
-        const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
-        const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
-        const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
-        const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
-        const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-        const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
-        const float gamma0 = acospi_q(VR_GAMMA_Q(lop0));
-        const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
-        const float gamma1 = acospi_q(VR_GAMMA_Q(lop1));
-        float light0, light1;
-#if VR_ABLATE & 1  // diagnostic: the LUT fetch's cost removed (wrong image)
-        light0 = beta0 + gamma0 + la.w;
-        light1 = beta1 + gamma1 + la.w;
-#else
-        if (TAME && VR_LUT_ZPAIR)  // the host binds a tame launch's LUT with its z-paired copy
-          fetch_small2_z(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
-                         axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
-        else
-          fetch_small2(P.lut, la, axis_lut<true>(beta0, P.lut.fny), axis_lut<true>(gamma0, P.lut.fnz),
-                       axis_lut<true>(beta1, P.lut.fny), axis_lut<true>(gamma1, P.lut.fnz), light0, light1);
-#endif
-        const float rl0 = refl * light0;
-        ir = fmaf(rl0 * L0.cr, P.color[0], ir);
-        ig = fmaf(rl0 * L0.cg, P.color[1], ig);
-        ib = fmaf(rl0 * L0.cb, P.color[2], ib);
-        const float rl1 = refl * light1;
-        ir = fmaf(rl1 * L1.cr, P.color[0], ir);
-        ig = fmaf(rl1 * L1.cg, P.color[1], ig);
-        ib = fmaf(rl1 * L1.cb, P.color[2], ib);
+#if VR_FAST_HYBRID
+    // the rsq-based shading everywhere, and where gamma is ill-conditioned (NEED) the sample's
+    // shading again with the oracle's normal and gamma cosines (per lane: the image does not depend
+    // on which lanes share a wave)
+    bool need = false;
+    const float ir0 = ir, ig0 = ig, ib0 = ib;
+    shade_fast<TAME, false, false, true>(P, g, pos, o, refl, ir, ig, ib, need);
+    if (__any(need)) {
+      float er = ir0, eg = ig0, eb = ib0;
+      bool unused = false;
+      shade_fast<TAME, true, true, false>(P, g, pos, o, refl, er, eg, eb, unused);
+      if (need) {
+        ir = er;
+        ig = eg;
+        ib = eb;
       }
     }
-    if constexpr (!TAME) for (; i + 1 < P.num_lights; i += 2) {
-      const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
-      const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
-      const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
-      const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
-      const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
-      const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-      const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
-      const float gamma0 = acospi_q(VR_GAMMA_Q(lop0));
-      const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
-      const float gamma1 = acospi_q(VR_GAMMA_Q(lop1));
-      const float light0 = lut_light<true>(P.lut, la, beta0, gamma0);
-      const float light1 = lut_light<true>(P.lut, la, beta1, gamma1);
-      const float rl0 = refl * light0;
-      ir = fmaf(rl0 * L0.cr, P.color[0], ir);
-      ig = fmaf(rl0 * L0.cg, P.color[1], ig);
-      ib = fmaf(rl0 * L0.cb, P.color[2], ib);
-      const float rl1 = refl * light1;
-      ir = fmaf(rl1 * L1.cr, P.color[0], ir);
-      ig = fmaf(rl1 * L1.cg, P.color[1], ig);
-      ib = fmaf(rl1 * L1.cb, P.color[2], ib);
-    }
-    if (i < P.num_lights) {
-      const DevLight L = light_at(P, i);
-      const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
-      const float dlo = dot3(lo, n);
-      const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-      const float beta = acospi_q(dlo * (rn * rsq_c(dot3(lo, lo))));
-      const float gamma = acospi_q(VR_GAMMA_Q(lop));
-      const float rl = refl * (TAME ? (VR_LUT_ZPAIR ? fetch_small_z(P.lut, la, axis_lut<true>(beta, P.lut.fny),
-                                                                   axis_lut<true>(gamma, P.lut.fnz))
-                                                    : fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
-                                                                  axis_lut<true>(gamma, P.lut.fnz)))
-                                    : lut_light<true>(P.lut, la, beta, gamma));
-      ir = fmaf(rl * L.cr, P.color[0], ir);
-      ig = fmaf(rl * L.cg, P.color[1], ig);
-      ib = fmaf(rl * L.cb, P.color[2], ib);
-    }
-#undef VR_GAMMA_Q
+#else
+    bool unused = false;
+    shade_fast<TAME, VR_FAST_NX, VR_FAST_GX, false>(P, g, pos, o, refl, ir, ig, ib, unused);
+#endif
   } else {
     // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
     // Correctly rounded 1/sqrtf, bit-identical to the oracle: the projections li - (li.n)n below
