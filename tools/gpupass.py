@@ -15,7 +15,7 @@ Steps ('|' separates variants, ',' environment assignments inside a variant):
   abl:SCENES:NAME=LIB[;ENV,..]|..  tools/shade_ablation.py parity of shading variants on the scenes
                                  (c2, metric, c4_main, c4_struct)                  -> ablation.json
   bench[:ARGS]                   the bench line (CPU baseline included unless ARGS say otherwise)
-                                                                                   -> bench.json
+                                 -> bench.json (the N-th bench step of a pass: benchN.json)
   kt[:ARGS]                      rocprofv3 --kernel-trace --stats of bench.py      -> ktN/ (N-th kt)
   pmc[:ARGS]                     tools/pmc.sh counter passes (one group per pass)  -> pmcN/ (N-th pmc)
   py:SCRIPT[ ARGS]               any python script of the tree (e.g. tools/tail_profile.py ...)
@@ -92,7 +92,7 @@ def main():
     run_name, steps = sys.argv[1], sys.argv[2:]
     out = os.path.join(ROOT, "gpurun_out", run_name)
     os.makedirs(out, exist_ok=True)
-    n_ab, n_kt, n_pmc, bench_args = 0, 0, 0, ""
+    n_ab, n_kt, n_pmc, n_bench, bench_args = 0, 0, 0, 0, ""
     for st in steps:
         kind, _, rest = st.partition(":")
         print(f"step {kind}: {rest[:120]}", flush=True)
@@ -113,10 +113,12 @@ def main():
             rc = run([PY, "-u", "tools/shade_ablation.py", os.path.join(out, "ablation.json")] + args,
                      os.path.join(out, "ablation.log"), 1100, env=e)
         elif kind == "bench":
-            with open(os.path.join(out, "bench.json"), "wb") as fh, open(os.path.join(out, "bench.err"), "wb") as fe:
+            n_bench += 1
+            tag = "bench" if n_bench == 1 else f"bench{n_bench}"
+            with open(os.path.join(out, tag + ".json"), "wb") as fh, open(os.path.join(out, tag + ".err"), "wb") as fe:
                 rc = subprocess.run(["timeout", "-k", "10", "500", PY, "bench.py"] + shlex.split(rest), cwd=ROOT,
                                     stdout=fh, stderr=fe).returncode
-            print(f"  bench rc={rc}", flush=True)
+            print(f"  {tag} rc={rc} ({rest or 'default'})", flush=True)
         elif kind == "kt":
             args = shlex.split(rest) or ["--steps", "10", "--warmup", "2", "--no-cpu-baseline", "--pipelined-streams",
                                          "0"]

@@ -565,10 +565,19 @@ __device__ __forceinline__ float exp_neg_rn(float x, bool small = false) {
 // 1 - __expf(-a * dx) (volumeRender_kernel.cu:456), both shading variants: the oracle's expf
 // (exp_neg_rn) -- x = a * dx rounded, then the exponential of its negation, as the oracle's
 // expf((-a) * dx) (negation is exact).
+// VR_OPACITY_EXP2 1 (a build switch, off by default): the reference's own form instead, __expf as
+// CUDA defines it -- exp2(x * log2 e) on the hardware exponential (v_exp_f32), the fast intrinsic of
+// volumeRender_kernel.cu:456 -- kept as the model of __expf; no fixture of the reference pins either
+// rounding (DESIGN.md s4 "opacity": the oracle's expf was chosen for its unbiased rounding).
+#ifndef VR_OPACITY_EXP2
+#define VR_OPACITY_EXP2 0
+#endif
 template <bool FAST>
 __device__ __forceinline__ float opacity(float a, float tstep, bool small = false) {
 #if VR_ABLATE & 8
   return a * tstep;
+#elif VR_OPACITY_EXP2
+  return 1.f - __builtin_amdgcn_exp2f(-(a * tstep) * 1.44269504088896341f);
 #else
   return 1.f - exp_neg_rn(a * tstep, small);
 #endif
