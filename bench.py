@@ -362,9 +362,12 @@ def main():
         # only when they were measured on this workload.
         try:
             with open(args.traffic_json) as fh:
-                tj = json.load(fh)
-            if (world == 1 and tj.get("workload") == result["config"]["workload"]
-                    and tj.get("kernel") == result["roofline"]["kernel"]):
+                tj_all = json.load(fh)
+            # one entry per measured workload (round 4: every BASELINE config), or a round-3 file
+            cands = tj_all.get("entries", [tj_all])
+            tj = next((e for e in cands if e.get("workload") == result["config"]["workload"]
+                       and e.get("kernel") == result["roofline"]["kernel"]), {})
+            if world == 1 and tj:
                 src = os.path.relpath(args.traffic_json, ROOT)
                 result["roofline"]["traffic"] = tj["bytes_per_launch"]
                 result["roofline"]["traffic_source"] = src + " (" + tj.get("method", "") + ")"
@@ -379,10 +382,28 @@ def main():
                                         "VALU instruction, MI355X_MICROARCH.md)"}
         except (OSError, ValueError, KeyError):
             pass
+        result["roofline"]["binding"] = binding_roof(result["roofline"], t_kernel_s)
         print(json.dumps(result), flush=True)
     vr.volumeRender("delete", h)
     if world > 1:
         dist.destroy_process_group()
+
+
+def binding_roof(rf, t_kernel_s):
+    """The roof nearest to binding the launch: the largest of the fractions that describe hardware
+    use -- the bytes the samples need (`fetched`), the HBM bytes the counters saw (FETCH_SIZE x 2 +
+    WRITE_SIZE, over 8 TB/s) and the VALU issue rate (over its wave64 peak).  The F-weighted sample
+    stream (`frac`) is a definitional figure (it charges F fetches to opacity-0 samples, which the
+    kernel skips; it reads above 1 at C5), so it is not a candidate."""
+    cands = {"fetched": rf["fetched"]["frac"]}
+    if rf.get("traffic"):
+        cands["hbm_traffic"] = round(rf["traffic"] / t_kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+    if rf.get("valu"):
+        cands["valu"] = rf["valu"]["frac"]
+    name = max(cands, key=cands.get)
+    return {"roof": name, "frac": cands[name], "candidates": cands,
+            "note": "max of the hardware-use fractions; none near 1 means the launch is latency-bound "
+                    "(waits the resident waves do not hide), DESIGN.md s5"}
 
 
 def cpu_share():

@@ -358,7 +358,7 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
     keys = ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT",
-            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS")
+            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS", "VR_NO_GDERIVED")
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
@@ -370,7 +370,9 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
                       ("nosched", {"VR_SCHED": "0"}), ("k2_sched", {"VR_DEPTH_LANES": "2", "VR_SCHED": "1"}),
                       ("k1_sched", {"VR_DEPTH_LANES": "1", "VR_SCHED": "1"}),
                       ("xcd_run2", {"VR_XCD_RUN": "2"}), ("k4_xcd_run4", {"VR_DEPTH_LANES": "4", "VR_XCD_RUN": "4"}),
-                      ("rot3", {"VR_BLOCK_ROT_ROWS": "3"}), ("k4_rot2", {"VR_DEPTH_LANES": "4", "VR_BLOCK_ROT_ROWS": "2"})]:
+                      ("rot3", {"VR_BLOCK_ROT_ROWS": "3"}), ("k4_rot2", {"VR_DEPTH_LANES": "4", "VR_BLOCK_ROT_ROWS": "2"}),
+                      ("noderived", {"VR_NO_GDERIVED": "1"}), ("k4_noderived", {"VR_DEPTH_LANES": "4", "VR_NO_GDERIVED": "1"}),
+                      ("k1_noderived_nogvec", {"VR_DEPTH_LANES": "1", "VR_NO_GDERIVED": "1", "VR_NO_GVEC": "1"})]:
         for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
@@ -382,6 +384,44 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
     assert base.max() > 0
     for name, img in imgs.items():
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
+    r.delete()
+
+
+@pytest.mark.parametrize("shade", ["fast", "exact"])
+def test_derived_lookup_gradient(monkeypatch, counter_clock, shade):
+    """Lookup gradient volumes that are MATLAB's gradient of the emission volume (Volume.grad, as
+    example1_grad.m builds them) are recognised on the device and their lookups computed from the
+    staged emission voxels (vr_last_march_flags bit 1); the image equals the gathering kernel's bit
+    for bit and the oracle's within the tolerance.  Gradient volumes that differ in one voxel by one
+    ulp are not derived: the kernel gathers them, and the image is the oracle's for those volumes."""
+    if shade == "exact":
+        monkeypatch.setenv("VR_EXACT_SHADE", "1")
+    else:
+        monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
+    from harness import install
+    from volume_renderer_amd import mex
+    tee = install(monkeypatch)
+    data = O.shell_volume(60)
+    v = vr.Volume(data)
+    r = ex1_renderer(v, res=(131, 97))
+    gx, gy, gz = v.grad()
+    r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = gx, gy, gz
+    derived = r.render()
+    assert mex.last_march_flags() & 1
+    monkeypatch.setenv("VR_NO_GDERIVED", "1")
+    gathered = r.render()
+    assert not (mex.last_march_flags() & 1)
+    monkeypatch.delenv("VR_NO_GDERIVED")
+    assert derived.max() > 0
+    assert np.array_equal(derived.view(np.uint32), gathered.view(np.uint32))
+    # one interior voxel of gy off by one ulp: not MATLAB's gradient any more
+    d2 = np.array(gy.Data, np.float32, copy=True)
+    k = (30, 31, 29)
+    d2[k] = np.nextafter(d2[k], np.float32(np.inf))
+    r.VolumeGradientY = vr.Volume(d2)
+    other = r.render()
+    assert not (mex.last_march_flags() & 1)
+    assert len(tee.renders) == 3  # each render checked against the oracle by the harness
     r.delete()
 
 

@@ -229,8 +229,15 @@ def test_committed_traffic_matches_bench_default_workload():
     path = bench._latest_traffic_json()
     with open(path) as fh:
         tj = json.load(fh)
-    assert tj["workload"] == bench.workload_name(1024, 1920, 1080, 2, "compute")
-    assert tj["bytes_per_launch"] > 0
+    entries = tj.get("entries", [tj])  # round 4: one entry per BASELINE config
+    want = {bench.workload_name(1024, 1920, 1080, 2, "compute"), bench.workload_name(1024, 1024, 768, 2, "compute"),
+            bench.workload_name(1024, 1920, 1080, 2, "lookup"), bench.workload_name(2048, 4096, 4096, 2, "compute")}
+    got = {e["workload"] for e in entries}
+    assert bench.workload_name(1024, 1920, 1080, 2, "compute") in got
+    if "entries" in tj:
+        assert want <= got, want - got
+    for e in entries:
+        assert e["bytes_per_launch"] > 0 and e["kernel"].startswith("vr::fast::march_kernel<")
 
 
 def test_cpu_share_is_positive():

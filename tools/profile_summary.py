@@ -8,7 +8,11 @@ HBM bytes: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts 64 B 
 here on stats_kernel, which reads every padded voxel once (known byte count).
 usage: tools/profile_summary.py gpurun_out/r13 profiles/round1 [WORKLOAD_STRING]
 The workload key defaults to the bench.json line of the run (bench.py matches it verbatim against
-its config.workload before it reports roofline.traffic)."""
+its config.workload before it reports roofline.traffic).
+Several configurations (round 4, one tools/gpupass.py pass with a bench and a pmc step per config):
+  tools/profile_summary.py --configs profiles/round4 PMC_DIR:BENCH_JSON[:NAME] ...
+writes traffic.json with one entry per config ({"entries": [...]}, bench.py picks the entry of its
+workload and kernel) and configs.json (each config's bench line with its counter-backed fractions)."""
 import csv
 import glob
 import json
@@ -18,6 +22,10 @@ import shutil
 import sys
 from collections import defaultdict
 
+if sys.argv[1] == "--configs":
+    import runpy
+    runpy.run_path(os.path.join(os.path.dirname(os.path.abspath(__file__)), "traffic_configs.py"), run_name="__main__")
+    sys.exit(0)
 run, out = sys.argv[1], sys.argv[2]
 workload = sys.argv[3] if len(sys.argv) > 3 else None
 if workload is None:

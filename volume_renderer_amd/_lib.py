@@ -99,6 +99,7 @@ SIGNATURES = [
     ("vr_last_error", c_char_p, []),
     ("vr_hip_errors", c_int64, [c_char_p, c_size_t]),
     ("vr_last_march_kernel", c_int, [c_char_p, c_size_t]),
+    ("vr_last_march_flags", c_int, []),
     ("vr_version", c_char_p, []),
 ]
 

@@ -75,6 +75,8 @@ hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int3
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
+hipError_t launch_gradient_check(const float *em, const float *gx, const float *gy, const float *gz,
+                                 const uint64_t dims[3], uint32_t *bad, hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
@@ -121,6 +123,11 @@ namespace vr {
 std::string &last_march_kernel() {
   static std::string name;
   return name;
+}
+// the launch options of that launch the kernel name does not show (vr_last_march_flags)
+int &last_march_flags() {
+  static int flags = 0;
+  return flags;
 }
 void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched) {
   char b[160];
@@ -292,6 +299,11 @@ struct TexUnit {
     std::shared_ptr<DevBuf> buf;
     const DevBuf *src[3] = {nullptr, nullptr, nullptr};
     uint64_t ver[3] = {0, 0, 0};
+    // derived_gradient: whether the three volumes are MATLAB's gradient of this emission buffer
+    const DevBuf *em = nullptr;
+    uint64_t em_ver = 0;
+    bool checked = false, derived = false;
+    uint32_t *d_bad = nullptr;  // the check's flag word on this device
   };
   std::map<int, GVec> gvec;  // per device (a multi-device group renders on every device)
 };
@@ -1181,6 +1193,45 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       }
     }
     if (G.buf) P.gvec = G.buf->ptr;
+    // derived_gradient (RenderParams::gderived): example1_grad.m renders with the gradient volumes
+    // Volume.grad() made from the emission volume itself.  Checked bit for bit on the device once
+    // per change of either (a pass over the volumes, 4 x 4 GiB at 1024^3: ~3 ms); then a staged
+    // sample computes its lookups' corner values from the emission voxels in its LDS slot (vr_stage.h
+    // cd_grad_lds) -- the same bits the gather reads.  VR_NO_GDERIVED=1: always gather (A/B, tests).
+    const BufPtr &be = g_tex.bind[g_tex.idx_em];
+    const bool dims_ok = be && be->dims[0] >= 4 && be->dims[1] >= 4 && be->dims[2] >= 4 &&
+                         be->dims[1] * be->dims[2] < 0xffffffffull;
+    if (dims_ok && !env_flag("VR_NO_GDERIVED")) {
+      const DevBuf *src[3] = {bx.get(), by.get(), bz.get()};
+      bool known = G.checked && G.em == be.get() && G.em_ver == be->version;
+      for (int i = 0; i < 3 && known; ++i) known = G.src[i] == src[i] && G.ver[i] == src[i]->version;
+      if (!known) G.checked = false;
+      if (!known && G.buf) {  // (the interleaved copy just checked or built records the same sources)
+        // (the flag word lives as long as the module state: no hipFree, which would wait for the
+        // whole device)
+        const hipError_t ea = G.d_bad ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&G.d_bad), sizeof(uint32_t));
+        if (ea == hipSuccess) {
+          uint32_t bad = 1u;
+          for (const BufPtr *b : {&be, &bx, &by, &bz}) wait_ready(*b, stream);
+          VR_HIP(hipMemsetAsync(G.d_bad, 0, sizeof(uint32_t), stream));
+          VR_HIP(vr::launch_gradient_check(be->ptr, bx->ptr, by->ptr, bz->ptr, be->dims, G.d_bad, stream));
+          VR_HIP(hipMemcpyAsync(&bad, G.d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+          VR_HIP(hipStreamSynchronize(stream));
+          G.em = be.get();
+          G.em_ver = be->version;
+          G.checked = true;
+          G.derived = bad == 0u;
+        } else {
+          vr_host::consume(ea, "hipMalloc (derived-gradient check; the lookups gather)");
+        }
+      }
+      P.gderived = (G.checked && G.derived && P.gvec) ? 1 : 0;
+    }
+    if (P.gderived) {
+      // the slot holds voxels i - 1 .. i + 2 of every lookup cell: a one-texel halo (before the
+      // chunk's drift margin, set_chunk_halo)
+      for (int i = 0; i < 3; ++i) P.tap_off[i] = 1.0625f;
+    }
   }
   if (fusable && march && F.mode <= 1 && !F.big && !P.steps) {
     *fusable = 1;
@@ -1234,6 +1285,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       P.block_rot = nb ? (uint32_t)(rot % nb) : 0u;
     }
     time_mark(h, 0, stream);
+    vr::last_march_flags() = (P.gderived ? 1 : 0);
     {
       const hipError_t e = fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream);
       if (e != hipSuccess) throw HipError{e, "the march kernel launch (launch_march_k)"};
@@ -2542,6 +2594,11 @@ int vr_last_march_kernel(char *buf, size_t buflen) {
     buf[n] = 0;
   }
   return VR_OK;
+}
+
+int vr_last_march_flags(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return vr::last_march_flags();
 }
 
 const char *vr_version(void) { return "libvrhip 0.1 gfx950 (MI355X) volume ray-marcher"; }

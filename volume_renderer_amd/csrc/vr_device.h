@@ -58,6 +58,11 @@ struct RenderParams {
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
   const float *gvec;              // lookup gradient interleaved (gx,gy,gz,0) x padded voxels, or null
+  // lookup gradient (MODE 2, shared axes): the three gradient volumes are MATLAB's gradient of the
+  // emission volume, bit for bit (checked on the device when either changes, vr_capi.hip
+  // derived_gradient), so a staged sample computes the eight corner values of each lookup from the
+  // emission voxels in its LDS slot instead of gathering them (vr_stage.h cd_grad_lds)
+  int32_t gderived;
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test

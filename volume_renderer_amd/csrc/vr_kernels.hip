@@ -387,6 +387,41 @@ hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, fl
   return hipGetLastError();
 }
 
+// Whether three lookup-gradient textures are MATLAB's gradient of the emission texture, bit for bit
+// (RenderParams::gderived): over the interior voxels of the apron layout (the borders replicate
+// them), gx == grad1 along dimension 2, gy along dimension 1, gz along dimension 3 -- the formulas of
+// gradient_kernel above, evaluated on the emission texture.  Any differing bit pattern (NaN payloads
+// included) stores 1 to *bad (a plain vector store from the lanes that differ).
+__global__ __launch_bounds__(256) void gradient_check_kernel(const float *__restrict__ em, const float *__restrict__ gx,
+                                                             const float *__restrict__ gy, const float *__restrict__ gz,
+                                                             uint32_t n0, uint32_t n1, uint32_t n2, uint32_t *bad) {
+  const uint64_t px = n0 + 2u, pxy = px * (n1 + 2u);
+  const uint32_t rows = n1 * n2;  // (host: below 2^32)
+  bool diff = false;
+  for (uint32_t r = blockIdx.x; r < rows; r += gridDim.x) {  // one (y, z) row per workgroup pass
+    const uint32_t k = r / n1, j = r - k * n1;
+    const uint64_t base = (uint64_t)(k + 1) * pxy + (uint64_t)(j + 1) * px + 1u;
+    for (uint32_t i = threadIdx.x; i < n0; i += blockDim.x) {
+      const uint64_t p = base + i;
+      diff = diff || __float_as_uint(gy[p]) != __float_as_uint(grad1(em, p, 1, i, n0)) ||
+             __float_as_uint(gx[p]) != __float_as_uint(grad1(em, p, px, j, n1)) ||
+             __float_as_uint(gz[p]) != __float_as_uint(grad1(em, p, pxy, k, n2));
+    }
+  }
+  if (diff) *bad = 1u;
+}
+
+hipError_t launch_gradient_check(const float *em, const float *gx, const float *gy, const float *gz,
+                                 const uint64_t dims[3], uint32_t *bad, hipStream_t s) {
+  const uint64_t rows = dims[1] * dims[2];
+  if (!rows || !dims[0]) return hipSuccess;
+  if (rows >= 0xffffffffull) return hipErrorInvalidValue;
+  const uint64_t blocks = rows < 65536 ? rows : 65536;
+  hipLaunchKernelGGL(gradient_check_kernel, dim3((unsigned)blocks), dim3(256), 0, s, em, gx, gy, gz,
+                     (uint32_t)dims[0], (uint32_t)dims[1], (uint32_t)dims[2], bad);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void interleave3_kernel(const float *__restrict__ a, const float *__restrict__ b,
                                                           const float *__restrict__ c, float4 *__restrict__ out,
                                                           uint64_t n) {

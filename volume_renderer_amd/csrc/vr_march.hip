@@ -298,6 +298,13 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
       g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
             fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
       g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
+    } else if (MODE == 2 && SHARE2 && P.gderived &&
+               __all(staged && (unsigned)(lx - 1) < (unsigned)(B.ex - 3) && (unsigned)(ly - 1) < (unsigned)(B.ey - 3) &&
+                     (unsigned)(lz - 1) < (unsigned)(B.ez - 3) && (unsigned)(ax.i - 1) <= (unsigned)(E.nx - 4) &&
+                     (unsigned)(ay.i - 1) <= (unsigned)(E.ny - 4) && (unsigned)(az.i - 1) <= (unsigned)(E.nz - 4))) {
+      // (wave-uniform over the shading lanes) the lookup gradient from the staged emission voxels:
+      // every shading lane's corners are interior voxels and voxels i - 1 .. i + 2 lie in the slot
+      g = cd_grad_lds(L, B, ac, ax.w, ay.w, az.w);
     } else if (MODE == 2 && SHARE2) {
       const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
       if (P.gvec)

@@ -170,6 +170,33 @@ __device__ __forceinline__ f3 half_grad_lds(const float *L, const Box &B, int ac
   return g;
 }
 
+// The lookup gradient of a sample whose three gradient volumes are MATLAB's gradient of the
+// emission volume (RenderParams::gderived; Volume.m:181-205 -> gradient(Data)): each corner value
+// of the lookups' 2x2x2 cell is the central difference (f(c + 1) - f(c - 1)) / 2 the gradient volume
+// holds at an interior voxel, taken from the staged emission voxels, and the corners are interpolated
+// exactly as fetch_vec interpolates the stored values (lerp x, then y, then z, per component) --
+// bit-identical to the gather for a cell whose corners are all interior (1 <= c <= n - 2 on every
+// axis: the one-sided ends are not derived here).  MATLAB's gx is the derivative along array
+// dimension 2 (slot rows, pitch px), gy along dimension 1 (slot x), gz along dimension 3 (planes).
+// The slot must hold voxels i - 1 .. i + 2 on every axis (the host's staging halo: tap_off >= 1).
+__device__ __forceinline__ f3 cd_grad_lds(const float *L, const Box &B, int ac, float wx, float wy, float wz) {
+  const int px = B.px, pxy = B.pxy;
+  // central difference along the axis of pitch s at slot word a (single precision, as MATLAB's)
+  auto cd = [&](int a, int s) { return (L[a + s] - L[a - s]) / 2.f; };
+  auto tri = [&](int s) {
+    const float c00 = lerp(cd(ac, s), cd(ac + 1, s), wx);
+    const float c10 = lerp(cd(ac + px, s), cd(ac + px + 1, s), wx);
+    const float c01 = lerp(cd(ac + pxy, s), cd(ac + pxy + 1, s), wx);
+    const float c11 = lerp(cd(ac + pxy + px, s), cd(ac + pxy + px + 1, s), wx);
+    return lerp(lerp(c00, c10, wy), lerp(c01, c11, wy), wz);
+  };
+  f3 g;
+  g.x = tri(px);
+  g.y = tri(1);
+  g.z = tri(pxy);
+  return g;
+}
+
 // Slot coordinates of a tap pair base and whether the cell [l, l+1] lies in the box along it.
 __device__ __forceinline__ int slot_coord(int i, int r) { return (int)((uint32_t)i + 1u - (uint32_t)r); }
 __device__ __forceinline__ bool in_box(int l, int e) {
