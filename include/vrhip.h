@@ -295,11 +295,6 @@ int64_t vr_hip_errors(char *buf, size_t buflen);
  * bench.py names the kernel it times with it and keys the profiler's counters to it. */
 int vr_last_march_kernel(char *buf, size_t buflen);
 
-/* Options of that launch its kernel name does not show (bit flags): 1 = the lookup gradient was
- * derived from the staged emission voxels (the gradient volumes are MATLAB's gradient of the
- * emission volume, checked bit for bit on the device).  Diagnostics and tests. */
-int vr_last_march_flags(void);
-
 /* Library build identification ("libvrhip <version> gfx950 ..."). */
 const char *vr_version(void);
 

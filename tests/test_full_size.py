@@ -39,10 +39,11 @@ THREADS = 16  # the GPU box's CPU share (os.cpu_count() there reports the whole 
 # the product may be at most half as far from the fp32 oracle (RMS over lit sampled channels) as the
 # fp32 oracle is from exact arithmetic (fp64), at every full-size config, default shading included
 MAX_RMS_RATIO = 0.5
-# and the unfloored SURVEY.md 8c fraction itself: the exact-op kernel meets the SURVEY's 99.9 %, the
-# default (fast) arithmetic at least 99.8 % at every config (measured 99.90-100 %)
+# and the unfloored SURVEY.md 8c fraction itself, the contract: >= 99.9 % of the sampled channels at
+# every config, for the exact-op kernel and the default (fast) arithmetic alike (round 4: the fast
+# shading takes gamma's cosine as the oracle's quotient near |cos| = 1)
 MIN_SURVEY_EXACT = 0.999
-MIN_SURVEY_FAST = 0.998
+MIN_SURVEY_FAST = 0.999
 EX1_LIGHTS = np.array([[500, 1000, 550, 0, 1, 1], [0, 550, 90, 1, 0.5, 1]], np.float32)
 EX3_LIGHT = np.array([[-15, 15, 0, 0.5, 0.5, 0.5]], np.float32)
 

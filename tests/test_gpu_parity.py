@@ -358,7 +358,7 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
     keys = ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT",
-            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS", "VR_NO_GDERIVED")
+            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS", "VR_SPLIT_FORCE")
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
@@ -371,8 +371,10 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
                       ("k1_sched", {"VR_DEPTH_LANES": "1", "VR_SCHED": "1"}),
                       ("xcd_run2", {"VR_XCD_RUN": "2"}), ("k4_xcd_run4", {"VR_DEPTH_LANES": "4", "VR_XCD_RUN": "4"}),
                       ("rot3", {"VR_BLOCK_ROT_ROWS": "3"}), ("k4_rot2", {"VR_DEPTH_LANES": "4", "VR_BLOCK_ROT_ROWS": "2"}),
-                      ("noderived", {"VR_NO_GDERIVED": "1"}), ("k4_noderived", {"VR_DEPTH_LANES": "4", "VR_NO_GDERIVED": "1"}),
-                      ("k1_noderived_nogvec", {"VR_DEPTH_LANES": "1", "VR_NO_GDERIVED": "1", "VR_NO_GVEC": "1"})]:
+                      ("k1_nogvec", {"VR_DEPTH_LANES": "1", "VR_NO_GVEC": "1"}),
+                      ("split_all", {"VR_SPLIT_FORCE": "1"}), ("split_third", {"VR_SPLIT_FORCE": "0.33"}),
+                      ("k2_split", {"VR_DEPTH_LANES": "2", "VR_SPLIT_FORCE": "1"}),
+                      ("k4_split", {"VR_DEPTH_LANES": "4", "VR_SPLIT_FORCE": "0.5"})]:
         for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
@@ -387,41 +389,37 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
     r.delete()
 
 
-@pytest.mark.parametrize("shade", ["fast", "exact"])
-def test_derived_lookup_gradient(monkeypatch, counter_clock, shade):
-    """Lookup gradient volumes that are MATLAB's gradient of the emission volume (Volume.grad, as
-    example1_grad.m builds them) are recognised on the device and their lookups computed from the
-    staged emission voxels (vr_last_march_flags bit 1); the image equals the gathering kernel's bit
-    for bit and the oracle's within the tolerance.  Gradient volumes that differ in one voxel by one
-    ulp are not derived: the kernel gathers them, and the image is the oracle's for those volumes."""
-    if shade == "exact":
-        monkeypatch.setenv("VR_EXACT_SHADE", "1")
-    else:
-        monkeypatch.delenv("VR_EXACT_SHADE", raising=False)
-    from harness import install
+@pytest.mark.parametrize("k", ["2", "4"])
+@pytest.mark.parametrize("scene", ["hg2", "lookup", "dense"])
+def test_chord_split_is_bit_identical(monkeypatch, counter_clock, scene, k):
+    """The chord split (vr_march.hip SCHED 4): the blocks' back halves marched by their
+    own workgroups from the replayed recurrence, their samples stored and composited onto the front
+    halves in order by split_composite_kernel -- the image of one pass, bit for bit, for every
+    fraction of split blocks, both gradient modes and the depth lanes of the full frame and of a
+    part.  `dense`: an opacity-heavy volume whose rays mostly stop early (in the front half, or in
+    the back half past B's own stop)."""
     from volume_renderer_amd import mex
+    from harness import install
+    monkeypatch.setenv("VR_DEPTH_LANES", k)
     tee = install(monkeypatch)
-    data = O.shell_volume(60)
+    data = O.shell_volume(64)
+    if scene == "dense":
+        data = np.asfortranarray(data * 2 + 0.02, dtype=np.float32)
     v = vr.Volume(data)
-    r = ex1_renderer(v, res=(131, 97))
-    gx, gy, gz = v.grad()
-    r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = gx, gy, gz
-    derived = r.render()
-    assert mex.last_march_flags() & 1
-    monkeypatch.setenv("VR_NO_GDERIVED", "1")
-    gathered = r.render()
-    assert not (mex.last_march_flags() & 1)
-    monkeypatch.delenv("VR_NO_GDERIVED")
-    assert derived.max() > 0
-    assert np.array_equal(derived.view(np.uint32), gathered.view(np.uint32))
-    # one interior voxel of gy off by one ulp: not MATLAB's gradient any more
-    d2 = np.array(gy.Data, np.float32, copy=True)
-    k = (30, 31, 29)
-    d2[k] = np.nextafter(d2[k], np.float32(np.inf))
-    r.VolumeGradientY = vr.Volume(d2)
-    other = r.render()
-    assert not (mex.last_march_flags() & 1)
-    assert len(tee.renders) == 3  # each render checked against the oracle by the harness
+    r = ex1_renderer(v, res=(133, 101))
+    if scene == "lookup":
+        r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
+    monkeypatch.setenv("VR_SPLIT", "0")
+    base = r.render()
+    assert not mex.last_march_kernel().endswith(", 4>")
+    monkeypatch.delenv("VR_SPLIT")
+    for f in ("1", "0.5", "0.1"):
+        monkeypatch.setenv("VR_SPLIT_FORCE", f)
+        img = r.render()
+        assert mex.last_march_kernel().endswith(", 4>"), (f, mex.last_march_kernel())
+        assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), (scene, k, f)
+    monkeypatch.delenv("VR_SPLIT_FORCE")
+    assert base.max() > 0 and len(tee.renders) == 4  # every render also checked against the oracle
     r.delete()
 
 

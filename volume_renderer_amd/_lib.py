@@ -10,7 +10,8 @@ import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("VR_LIB_PATH") or os.path.join(_HERE, "libvrhip.so")  # override: A/B builds
+_DEFAULT_PATH = os.path.join(_HERE, "libvrhip.so")
+LIB_PATH = os.environ.get("VR_LIB_PATH") or _DEFAULT_PATH  # override: A/B builds
 
 VR_OK = 0
 VR_HOST = 0
@@ -99,7 +100,6 @@ SIGNATURES = [
     ("vr_last_error", c_char_p, []),
     ("vr_hip_errors", c_int64, [c_char_p, c_size_t]),
     ("vr_last_march_kernel", c_int, [c_char_p, c_size_t]),
-    ("vr_last_march_flags", c_int, []),
     ("vr_version", c_char_p, []),
 ]
 
@@ -120,6 +120,8 @@ def lib():
                               "(make -C volume_renderer_amd/csrc)")
         handle = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            if LIB_PATH != _DEFAULT_PATH and not hasattr(handle, name):
+                continue  # an A/B build of an earlier tree (VR_LIB_PATH) may predate a diagnostic entry
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -25,6 +25,7 @@
 #include <array>
 #include <sstream>
 #include <string>
+#include <queue>
 #include <vector>
 
 #include "../../include/vrhip.h"
@@ -75,9 +76,8 @@ hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int3
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
-hipError_t launch_gradient_check(const float *em, const float *gx, const float *gy, const float *gz,
-                                 const uint64_t dims[3], uint32_t *bad, hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
+hipError_t launch_split_composite(const RenderParams &P, uint32_t nrays, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
 hipError_t launch_synth_shell(float *out, uint64_t n, uint64_t z_first, uint64_t nz, hipStream_t s);
@@ -124,11 +124,7 @@ std::string &last_march_kernel() {
   static std::string name;
   return name;
 }
-// the launch options of that launch the kernel name does not show (vr_last_march_flags)
-int &last_march_flags() {
-  static int flags = 0;
-  return flags;
-}
+
 void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched) {
   char b[160];
   auto tf = [](bool v) { return v ? "true" : "false"; };
@@ -253,6 +249,18 @@ struct vr_context {
     uint32_t *h_order = nullptr;  // pinned: a host-computed order (VR_SCHED_SHIFT / VR_SCHED_ROWS)
     hipEvent_t copied = nullptr;
     bool copy_pending = false, decided = false, tail = false;
+    // chord split of the heaviest blocks (split_choose / split_attach; frames without a tail
+    // schedule): the blocks' back halves (d_split_list), the block -> slot map (d_split_of, -1: not
+    // split), per split ray the back half's records and the hand-over state; pinned plan staging
+    bool split_stale = false;  // a plan chosen from new durations, not yet attached
+    std::vector<uint32_t> split_plan;
+    uint32_t split_n = 0, split_slots = 0, split_cap = 0;
+    uint32_t *d_split_list = nullptr, *h_split_list = nullptr;
+    int32_t *d_split_of = nullptr, *h_split_of = nullptr;
+    float *d_split_rec = nullptr, *d_split_hand = nullptr;
+    int32_t *d_split_cnt = nullptr;
+    uint32_t *d_split_pix = nullptr;
+    size_t split_rec_bytes = 0;
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -299,11 +307,6 @@ struct TexUnit {
     std::shared_ptr<DevBuf> buf;
     const DevBuf *src[3] = {nullptr, nullptr, nullptr};
     uint64_t ver[3] = {0, 0, 0};
-    // derived_gradient: whether the three volumes are MATLAB's gradient of this emission buffer
-    const DevBuf *em = nullptr;
-    uint64_t em_ver = 0;
-    bool checked = false, derived = false;
-    uint32_t *d_bad = nullptr;  // the check's flag word on this device
   };
   std::map<int, GVec> gvec;  // per device (a multi-device group renders on every device)
 };
@@ -611,6 +614,7 @@ struct Frame {
   bool ab_alias = false, big = false, share = false;
   bool degenerate = false;
   vr_context::Schedule *sched_copy = nullptr;  // a timed full-frame launch: copy its durations back
+  vr_context::Schedule *sched = nullptr;       // the launch shape's schedule (attach_schedule)
 };
 
 
@@ -938,6 +942,10 @@ bool want_schedule(const vr::RenderParams &P) {
   return env_flag("VR_SCHED") || short_launch(P) || !env_flag_off("VR_SCHED_FULL");
 }
 
+std::vector<uint32_t> split_choose(const uint32_t *cost, uint32_t nb, uint32_t W);
+hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uint32_t nb,
+                        const std::vector<uint32_t> *chosen, hipStream_t stream);
+
 // launch_order's tail argument: (tail_pct << 32) | resident workgroups; tail_pct 0 = heavy-first.
 uint64_t wg_tail_arg(uint32_t tail_pct) {
   return (uint64_t)tail_pct << 32 | (uint64_t)(device_wave_slots() / 16 * 6);
@@ -957,6 +965,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   std::snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%d/%u/%p/%s", K, P.width, P.height, P.part, P.num_parts,
                 P.block_cols, F.mode, P.wide_slot, P.fast_shade, nb, (void *)stream, extra);
   vr_context::Schedule &S = h->sched[key];
+  F.sched = &S;
   if (!S.d_cost && nb) {
     hipError_t e = hipMalloc(&S.d_cost, nb * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&S.d_order, nb * sizeof(uint32_t));
@@ -1025,6 +1034,12 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
       S.tail = rows || shift > 0.0 || (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
       S.decided = true;
       S.order_stale = true;
+      // the chord split of the following unscheduled frames, chosen now: h_cost is rewritten by the
+      // next measurement's copy
+      if (env_flag("VR_SPLIT")) {
+        S.split_plan = split_choose(S.h_cost, nb, (uint32_t)(device_wave_slots() / 16 * 5));
+        S.split_stale = true;
+      }
       // workgroup wg is tile block (wg % nbx, wg / nbx) (vr_march.hip march_kernel)
       const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
       const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
@@ -1089,6 +1104,160 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   // none for a full frame, whose first blocks are only the heavy ones
   P.prio_blocks = P.sched_full ? 0u : (uint32_t)(device_wave_slots() / 4);
   if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
+  return hipSuccess;
+}
+
+// ---- chord split (DESIGN.md s8 "chord split"; vr_march.hip SCHED 4) ------------------------------
+// A block whose waves march rays crossing both shell walls lasts up to ten times the median and, in
+// row-major order, may start late and end alone (the frame's ramp-down).  Such a block is marched
+// twice at once: its front halves (A) in the block's own place and its back halves (B) among the
+// first workgroups of the launch; split_composite_kernel joins them in sample order afterwards --
+// bit-identical to one pass.
+#ifndef VR_SPLIT_MIN_FRAC
+#define VR_SPLIT_MIN_FRAC 0.10  // split only blocks lasting at least this fraction of the packed frame
+#endif
+#ifndef VR_SPLIT_GAIN
+#define VR_SPLIT_GAIN 0.97  // ... and only if the simulated frame shrinks below this fraction
+#endif
+
+// List scheduling of blocks with durations d in `order` over W workgroup slots (the dispatcher gives
+// the next block to the first free slot); per block its end time; returns the makespan.
+double sim_list(const std::vector<double> &d, const std::vector<uint32_t> &order, uint32_t W,
+                std::vector<double> *end) {
+  std::priority_queue<double, std::vector<double>, std::greater<double>> free_at;
+  for (uint32_t i = 0; i < W; ++i) free_at.push(0.0);
+  double span = 0.0;
+  for (uint32_t b : order) {
+    const double t0 = free_at.top();
+    free_at.pop();
+    const double t1 = t0 + d[b];
+    if (end) (*end)[b] = t1;
+    free_at.push(t1);
+    span = std::max(span, t1);
+  }
+  return span;
+}
+
+// The blocks to split, from the durations of the last measured launch (row-major order): those that
+// end after the packed frame (sum / W) in a simulation of the launch and last at least
+// VR_SPLIT_MIN_FRAC of it, over two rounds (a split moves the other blocks); none unless the
+// simulated split frame is shorter by VR_SPLIT_GAIN.  At most nb / 8 blocks.
+std::vector<uint32_t> split_choose(const uint32_t *cost, uint32_t nb, uint32_t W) {
+  std::vector<double> d(nb);
+  double sum = 0.0;
+  for (uint32_t i = 0; i < nb; ++i) sum += (d[i] = (double)cost[i]);
+  const double packed = sum / std::max<uint32_t>(W, 1u);
+  double min_frac = VR_SPLIT_MIN_FRAC, gain = VR_SPLIT_GAIN;  // (A/B: VR_SPLIT_MIN_FRAC, VR_SPLIT_GAIN)
+  if (const char *ev = std::getenv("VR_SPLIT_MIN_FRAC")) min_frac = std::atof(ev);
+  if (const char *ev = std::getenv("VR_SPLIT_GAIN")) gain = std::atof(ev);
+  std::vector<uint32_t> order(nb);
+  for (uint32_t i = 0; i < nb; ++i) order[i] = i;
+  std::vector<double> end(nb);
+  const double span0 = sim_list(d, order, W, &end);
+  std::vector<char> split(nb, 0);
+  std::vector<uint32_t> chosen;
+  double span = span0;
+  for (int round = 0; round < 2; ++round) {
+    for (uint32_t i = 0; i < nb && chosen.size() < nb / 8; ++i)
+      if (!split[i] && end[i] > packed && d[i] >= min_frac * packed) {
+        split[i] = 1;
+        chosen.push_back(i);
+      }
+    // the split launch: the back halves first, then every block in row-major order (halved if split)
+    std::vector<double> dd(d);
+    std::vector<uint32_t> ord2;
+    for (size_t j = 0; j < chosen.size(); ++j) {
+      dd.push_back(d[chosen[j]] * 0.5);
+      ord2.push_back(nb + (uint32_t)j);
+    }
+    for (uint32_t i = 0; i < nb; ++i) {
+      if (split[i]) dd[i] = d[i] * 0.5;
+      ord2.push_back(i);
+    }
+    std::vector<double> end2(dd.size());
+    span = sim_list(dd, ord2, W, &end2);
+    for (uint32_t i = 0; i < nb; ++i) end[i] = end2[i];
+  }
+  if (env_flag("VR_SPLIT_DEBUG"))  // diagnostics: the simulation behind the decision
+    std::fprintf(stderr, "split_choose: %u blocks, W %u, packed %.0f, row-major span %.0f, %zu split -> span %.0f\n",
+                 nb, W, packed, span0, chosen.size(), span);
+  if (chosen.empty() || span > gain * span0) chosen.clear();
+  return chosen;
+}
+
+// Fill S's split buffers for `chosen` (tile blocks of a K-lane launch of nb blocks; null: keep the
+// last plan) and attach them to P.  A split ray's records hold its back half: at most half the
+// longest chord of its wave in samples plus the drift of the t recurrence (t += tstep rounds by up
+// to ulp(t) / 2 per sample).
+hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uint32_t nb,
+                        const std::vector<uint32_t> *chosen, hipStream_t stream) {
+  if (chosen) {  // a new plan
+    const uint32_t n = (uint32_t)chosen->size();
+    if (!S.d_split_of) {
+      hipError_t e = hipMalloc(reinterpret_cast<void **>(&S.d_split_of), nb * sizeof(int32_t));
+      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_split_of), nb * sizeof(int32_t));
+      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_list), nb * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_split_list), nb * sizeof(uint32_t));
+      if (e != hipSuccess) return e;
+    }
+    double pmax = 0.0, diag = 0.0;
+    for (int i = 0; i < 3; ++i) {
+      pmax = std::max(pmax, (double)std::fabs(P.eye[i]) + std::fabs(P.bmin[i]));
+      diag += 4.0 * (double)P.bmin[i] * P.bmin[i];
+    }
+    diag = std::sqrt(diag);
+    const double est = diag / (double)P.tstep + 2.0;
+    const double drift = est * std::ldexp(1.0, std::ilogb(pmax + diag) - 24) / (double)P.tstep;
+    const uint32_t cap = (uint32_t)std::min(est * 0.5 + drift + 64.0, (double)P.max_steps);
+    const uint32_t rays = n * 4u * (64u / (uint32_t)K);
+    const size_t rec_bytes = (size_t)rays * cap * 4 * sizeof(float);
+    if (rays > S.split_slots || rec_bytes > S.split_rec_bytes) {
+      // grown rarely (a plan with more split rays): a launch in flight on this stream may still read
+      // the old buffers -- wait for it before they go
+      VR_HIP(hipStreamSynchronize(stream));
+      for (void *q : {(void *)S.d_split_rec, (void *)S.d_split_hand, (void *)S.d_split_cnt, (void *)S.d_split_pix})
+        if (q) (void)hipFree(q);
+      S.d_split_rec = S.d_split_hand = nullptr;
+      S.d_split_cnt = nullptr;
+      S.d_split_pix = nullptr;
+      S.split_slots = 0;
+      S.split_rec_bytes = 0;
+      S.split_n = 0;
+      const uint32_t rays_alloc = rays + rays / 4;
+      const size_t bytes = rec_bytes + rec_bytes / 4;
+      hipError_t e = hipMalloc(reinterpret_cast<void **>(&S.d_split_rec), bytes);
+      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_hand), rays_alloc * sizeof(float));
+      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_cnt), rays_alloc * sizeof(int32_t));
+      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_pix), rays_alloc * sizeof(uint32_t));
+      if (e != hipSuccess) return e;
+      S.split_slots = rays_alloc;
+      S.split_rec_bytes = bytes;
+    }
+    // the pinned plan buffers are rewritten only after their previous copy has run
+    VR_HIP(hipStreamSynchronize(stream));
+    for (uint32_t i = 0; i < nb; ++i) S.h_split_of[i] = -1;
+    for (uint32_t j = 0; j < n; ++j) {
+      S.h_split_list[j] = (*chosen)[j];
+      S.h_split_of[(*chosen)[j]] = (int32_t)j;
+    }
+    VR_HIP(hipMemcpyAsync(S.d_split_of, S.h_split_of, nb * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+    if (n) VR_HIP(hipMemcpyAsync(S.d_split_list, S.h_split_list, n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    S.split_n = n;
+    S.split_cap = cap;
+    S.split_stale = false;
+  }
+  if (!S.split_n) return hipSuccess;
+  P.split_n = S.split_n;
+  P.split_list = S.d_split_list;
+  P.split_of = S.d_split_of;
+  P.split_rec = S.d_split_rec;
+  P.split_cnt = S.d_split_cnt;
+  P.split_pix = S.d_split_pix;
+  P.split_hand = S.d_split_hand;
+  P.split_cap = S.split_cap;
+  // B stops once its own opacity passes thr by more than the rounding of two fp32 recurrences can
+  // set it apart from the ray's true opacity (at least B's in exact arithmetic); never for thr near 1
+  P.split_thr = P.thr + 4e-3f < 1.f ? P.thr + 4e-3f : 2.f;
   return hipSuccess;
 }
 
@@ -1193,45 +1362,6 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       }
     }
     if (G.buf) P.gvec = G.buf->ptr;
-    // derived_gradient (RenderParams::gderived): example1_grad.m renders with the gradient volumes
-    // Volume.grad() made from the emission volume itself.  Checked bit for bit on the device once
-    // per change of either (a pass over the volumes, 4 x 4 GiB at 1024^3: ~3 ms); then a staged
-    // sample computes its lookups' corner values from the emission voxels in its LDS slot (vr_stage.h
-    // cd_grad_lds) -- the same bits the gather reads.  VR_NO_GDERIVED=1: always gather (A/B, tests).
-    const BufPtr &be = g_tex.bind[g_tex.idx_em];
-    const bool dims_ok = be && be->dims[0] >= 4 && be->dims[1] >= 4 && be->dims[2] >= 4 &&
-                         be->dims[1] * be->dims[2] < 0xffffffffull;
-    if (dims_ok && !env_flag("VR_NO_GDERIVED")) {
-      const DevBuf *src[3] = {bx.get(), by.get(), bz.get()};
-      bool known = G.checked && G.em == be.get() && G.em_ver == be->version;
-      for (int i = 0; i < 3 && known; ++i) known = G.src[i] == src[i] && G.ver[i] == src[i]->version;
-      if (!known) G.checked = false;
-      if (!known && G.buf) {  // (the interleaved copy just checked or built records the same sources)
-        // (the flag word lives as long as the module state: no hipFree, which would wait for the
-        // whole device)
-        const hipError_t ea = G.d_bad ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&G.d_bad), sizeof(uint32_t));
-        if (ea == hipSuccess) {
-          uint32_t bad = 1u;
-          for (const BufPtr *b : {&be, &bx, &by, &bz}) wait_ready(*b, stream);
-          VR_HIP(hipMemsetAsync(G.d_bad, 0, sizeof(uint32_t), stream));
-          VR_HIP(vr::launch_gradient_check(be->ptr, bx->ptr, by->ptr, bz->ptr, be->dims, G.d_bad, stream));
-          VR_HIP(hipMemcpyAsync(&bad, G.d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-          VR_HIP(hipStreamSynchronize(stream));
-          G.em = be.get();
-          G.em_ver = be->version;
-          G.checked = true;
-          G.derived = bad == 0u;
-        } else {
-          vr_host::consume(ea, "hipMalloc (derived-gradient check; the lookups gather)");
-        }
-      }
-      P.gderived = (G.checked && G.derived && P.gvec) ? 1 : 0;
-    }
-    if (P.gderived) {
-      // the slot holds voxels i - 1 .. i + 2 of every lookup cell: a one-texel halo (before the
-      // chunk's drift margin, set_chunk_halo)
-      for (int i = 0; i < 3; ++i) P.tap_off[i] = 1.0625f;
-    }
   }
   if (fusable && march && F.mode <= 1 && !F.big && !P.steps) {
     *fusable = 1;
@@ -1257,7 +1387,33 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
          VR_K8(vr::fast::launch_march_k8, vr::fast::launch_march_k4)}};
     const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
     // (the exact-arithmetic variant is a parity reference: built without the scheduled kernels)
-    if (!P.steps && K > 1 && P.fast_shade && want_schedule(P)) VR_HIP(attach_schedule(h, P, F, K, stream, ""));
+    // chord split (split_choose; opt-in, VR_SPLIT=1 -- measured slower on MI355X): an
+    // unscheduled full frame whose last measured durations show blocks ending after the packed frame.
+    // VR_SPLIT_FORCE=f (tests): any eligible launch, unscheduled, with a pseudo-random fraction f of
+    // its blocks split (all: f >= 1)
+    const bool can_split = K > 1 && P.fast_shade && P.tame && F.mode >= 1 && F.ab_alias && !F.big && !P.wide_slot &&
+                           P.views <= 1 && !P.steps;
+    const char *force = can_split ? std::getenv("VR_SPLIT_FORCE") : nullptr;
+    if (force) {
+      static const blocks_fn fbf[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
+                                       VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
+      const uint32_t nb = fbf[ki](P);
+      char key[300];
+      std::snprintf(key, sizeof key, "split-force/%d/%d/%d/%d/%d/%u/%p", K, P.width, P.height, P.part, P.num_parts, nb,
+                    (void *)stream);
+      vr_context::Schedule &S = h->sched[key];
+      const double f = std::atof(force);
+      std::vector<uint32_t> ch;
+      for (uint32_t i = 0; i < nb; ++i)
+        if (f >= 1.0 || (double)((i * 2654435761u) >> 8 & 0xffffu) < f * 65536.0) ch.push_back(i);
+      VR_HIP(split_attach(S, P, K, nb, &ch, stream));
+    } else {
+      if (!P.steps && K > 1 && P.fast_shade && want_schedule(P)) VR_HIP(attach_schedule(h, P, F, K, stream, ""));
+      if (can_split && env_flag("VR_SPLIT") && !P.wg_order && F.sched && F.sched->decided && !F.sched->tail) {
+        vr_context::Schedule &S = *F.sched;
+        VR_HIP(split_attach(S, P, K, S.blocks, S.split_stale ? &S.split_plan : nullptr, stream));
+      }
+    }
     if (P.views > 1) {
       static const blocks_fn vfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
                                         vr::fast::march_blocks_k4,
@@ -1285,11 +1441,12 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       P.block_rot = nb ? (uint32_t)(rot % nb) : 0u;
     }
     time_mark(h, 0, stream);
-    vr::last_march_flags() = (P.gderived ? 1 : 0);
     {
       const hipError_t e = fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream);
       if (e != hipSuccess) throw HipError{e, "the march kernel launch (launch_march_k)"};
     }
+    if (P.split_n)  // the split rays' back halves composited onto their front halves, in order
+      VR_HIP(vr::launch_split_composite(P, P.split_n * 4u * (64u / (uint32_t)K), stream));
     time_mark(h, 1, stream);
     if (F.sched_copy) {  // a timed full frame: its block durations to the host, for the tail test
       vr_context::Schedule &S = *F.sched_copy;
@@ -2594,11 +2751,6 @@ int vr_last_march_kernel(char *buf, size_t buflen) {
     buf[n] = 0;
   }
   return VR_OK;
-}
-
-int vr_last_march_flags(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  return vr::last_march_flags();
 }
 
 const char *vr_version(void) { return "libvrhip 0.1 gfx950 (MI355X) volume ray-marcher"; }

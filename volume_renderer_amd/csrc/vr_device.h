@@ -58,11 +58,6 @@ struct RenderParams {
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
   const float *gvec;              // lookup gradient interleaved (gx,gy,gz,0) x padded voxels, or null
-  // lookup gradient (MODE 2, shared axes): the three gradient volumes are MATLAB's gradient of the
-  // emission volume, bit for bit (checked on the device when either changes, vr_capi.hip
-  // derived_gradient), so a staged sample computes the eight corner values of each lookup from the
-  // emission voxels in its LDS slot instead of gathering them (vr_stage.h cd_grad_lds)
-  int32_t gderived;
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test
@@ -96,6 +91,21 @@ struct RenderParams {
                                   // 2 following the last measured order without timing
   uint32_t prio_blocks;           // scheduled launch: the first prio_blocks workgroups (the longest)
                                   // run at raised wave priority
+  // chord split of the heaviest tile blocks (DESIGN.md s8 "chord split"; march_kernel SPLIT): the
+  // first split_n workgroups march the back halves of the blocks split_list[0 .. split_n) ("B":
+  // from sample index n_split on, each sample's premultiplied colour and opacity stored to
+  // split_rec, nothing composited into the image), the rest march the frame, the split blocks'
+  // rays only up to n_split ("A"); split_composite_kernel then composites each split ray's stored
+  // samples onto its A state in order, with the early exit -- the sequential loop's arithmetic.
+  // n_split is per wave: half the longest chord (in samples) of its rays, the same in A and B.
+  const uint32_t *split_list;     // B workgroup b -> tile block
+  const int32_t *split_of;        // tile block -> split slot (index into split_list), or -1
+  float *split_rec;               // per split ray (slot x wave x ray): split_cap records of 4 floats
+  int32_t *split_cnt;             // per split ray: records B stored (-1: no ray)
+  uint32_t *split_pix;            // per split ray: its output pixel index (B), or ~0
+  float *split_hand;              // per split ray: A's opacity when it handed over, or -1
+  uint32_t split_n, split_cap;
+  float split_thr;                // B's own stop: its local opacity past thr + margin
   unsigned long long *steps;      // optional sample counter
   // sort-last slab launch (vr_render_slab): owned normalized z range [slab_z0,
   // slab_z1), the margin of the chunk ownership test, the resident padded planes [slab_pk0,

@@ -387,38 +387,55 @@ hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, fl
   return hipGetLastError();
 }
 
-// Whether three lookup-gradient textures are MATLAB's gradient of the emission texture, bit for bit
-// (RenderParams::gderived): over the interior voxels of the apron layout (the borders replicate
-// them), gx == grad1 along dimension 2, gy along dimension 1, gz along dimension 3 -- the formulas of
-// gradient_kernel above, evaluated on the emission texture.  Any differing bit pattern (NaN payloads
-// included) stores 1 to *bad (a plain vector store from the lanes that differ).
-__global__ __launch_bounds__(256) void gradient_check_kernel(const float *__restrict__ em, const float *__restrict__ gx,
-                                                             const float *__restrict__ gy, const float *__restrict__ gz,
-                                                             uint32_t n0, uint32_t n1, uint32_t n2, uint32_t *bad) {
-  const uint64_t px = n0 + 2u, pxy = px * (n1 + 2u);
-  const uint32_t rows = n1 * n2;  // (host: below 2^32)
-  bool diff = false;
-  for (uint32_t r = blockIdx.x; r < rows; r += gridDim.x) {  // one (y, z) row per workgroup pass
-    const uint32_t k = r / n1, j = r - k * n1;
-    const uint64_t base = (uint64_t)(k + 1) * pxy + (uint64_t)(j + 1) * px + 1u;
-    for (uint32_t i = threadIdx.x; i < n0; i += blockDim.x) {
-      const uint64_t p = base + i;
-      diff = diff || __float_as_uint(gy[p]) != __float_as_uint(grad1(em, p, 1, i, n0)) ||
-             __float_as_uint(gx[p]) != __float_as_uint(grad1(em, p, px, j, n1)) ||
-             __float_as_uint(gz[p]) != __float_as_uint(grad1(em, p, pxy, k, n2));
-    }
+// Chord split (vr_march.hip SCHED 4, RenderParams::split_*): per split ray, its back half's stored
+// samples composited onto the front half's result in sample order -- the reference's loop body
+// (volumeRender_kernel.cu:476-486: sum += (1 - sum.a) * col, stop once sum.a > thr) on the values the
+// march computed; the records hold exactly the samples that exist (t <= tfar, under max_steps) and
+// the ones of empty-chunk leaps (which add exactly nothing) are left out.  One lane per ray, its
+// records streamed 8 at a time.  A record count of -2 (capacity exceeded; the host sizes the
+// buffer so that it cannot happen) marks the pixel NaN rather than leave it silently wrong.
+__global__ __launch_bounds__(256) void split_composite_kernel(const RenderParams P, uint32_t nrays) {
+  const uint32_t id = blockIdx.x * 256u + threadIdx.x;
+  if (id >= nrays) return;
+  const uint32_t pix = P.split_pix[id];
+  const float hand = P.split_hand[id];
+  const int cnt = P.split_cnt[id];
+  if (pix == 0xffffffffu || !(hand >= 0.f)) return;  // no ray, or its front half stopped it
+  const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
+  float *o = P.out + pix;
+  if (cnt < 0) {
+    o[0] = o[plane] = o[2 * plane] = __builtin_nanf("");
+    return;
   }
-  if (diff) *bad = 1u;
+  float sr = o[0], sg = o[plane], sb = o[2 * plane], sa = hand;
+  const float4 *rec = reinterpret_cast<const float4 *>(P.split_rec) + (size_t)id * P.split_cap;
+  const float thr = P.thr;
+  for (int j0 = 0; j0 < cnt; j0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = j0 + i < cnt ? rec[j0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bool stop = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (!stop && j0 + i < cnt) {
+        const float om = 1.f - sa;
+        sr = fmaf(om, v[i].x, sr);
+        sg = fmaf(om, v[i].y, sg);
+        sb = fmaf(om, v[i].z, sb);
+        sa = fmaf(om, v[i].w, sa);
+        stop = sa > thr;
+      }
+    }
+    if (stop) break;
+  }
+  o[0] = sr;
+  o[plane] = sg;
+  o[2 * plane] = sb;
 }
 
-hipError_t launch_gradient_check(const float *em, const float *gx, const float *gy, const float *gz,
-                                 const uint64_t dims[3], uint32_t *bad, hipStream_t s) {
-  const uint64_t rows = dims[1] * dims[2];
-  if (!rows || !dims[0]) return hipSuccess;
-  if (rows >= 0xffffffffull) return hipErrorInvalidValue;
-  const uint64_t blocks = rows < 65536 ? rows : 65536;
-  hipLaunchKernelGGL(gradient_check_kernel, dim3((unsigned)blocks), dim3(256), 0, s, em, gx, gy, gz,
-                     (uint32_t)dims[0], (uint32_t)dims[1], (uint32_t)dims[2], bad);
+hipError_t launch_split_composite(const RenderParams &P, uint32_t nrays, hipStream_t s) {
+  if (!nrays) return hipSuccess;
+  hipLaunchKernelGGL(split_composite_kernel, dim3((nrays + 255) / 256), dim3(256), 0, s, P, nrays);
   return hipGetLastError();
 }
 

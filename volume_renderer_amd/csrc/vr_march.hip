@@ -298,13 +298,6 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
       g.z = fetch_at<BIG>(E, L, B, sxy && in_box(lzp, B.ez), axy + lzp * B.pxy, ax, ay, azp) -
             fetch_at<BIG>(E, L, B, sxy && in_box(lzm, B.ez), axy + lzm * B.pxy, ax, ay, azm);
       g = mk(g.x * 0.5f, g.y * 0.5f, g.z * 0.5f);
-    } else if (MODE == 2 && SHARE2 && P.gderived &&
-               __all(staged && (unsigned)(lx - 1) < (unsigned)(B.ex - 3) && (unsigned)(ly - 1) < (unsigned)(B.ey - 3) &&
-                     (unsigned)(lz - 1) < (unsigned)(B.ez - 3) && (unsigned)(ax.i - 1) <= (unsigned)(E.nx - 4) &&
-                     (unsigned)(ay.i - 1) <= (unsigned)(E.ny - 4) && (unsigned)(az.i - 1) <= (unsigned)(E.nz - 4))) {
-      // (wave-uniform over the shading lanes) the lookup gradient from the staged emission voxels:
-      // every shading lane's corners are interior voxels and voxels i - 1 .. i + 2 lie in the slot
-      g = cd_grad_lds(L, B, ac, ax.w, ay.w, az.w);
     } else if (MODE == 2 && SHARE2) {
       const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
       if (P.gvec)
@@ -336,14 +329,17 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
 // Front-to-back compositing of one sample and the march recurrences of volumeRender_kernel.cu:
 // 476-492, in the reference's order: early exit on sum.a > thr before t > tfar; pos += step only
 // while the ray goes on.
-__device__ __forceinline__ void composite(const RenderParams &P, Ray &R, float r, float gg, float b, float alpha) {
+// thr / cap: the exit threshold and the sample cap (P.thr / P.max_steps; a chord split's halves
+// use their own, march SPLIT).
+__device__ __forceinline__ void composite(const RenderParams &P, Ray &R, float r, float gg, float b, float alpha,
+                                          float thr, int cap) {
   const float om = 1.f - R.sa;
   R.sr = fmaf(om, r, R.sr);
   R.sg = fmaf(om, gg, R.sg);
   R.sb = fmaf(om, b, R.sb);
   R.sa = fmaf(om, alpha, R.sa);
   ++R.nsteps;
-  if (R.sa > P.thr || R.nsteps >= P.max_steps) {
+  if (R.sa > thr || R.nsteps >= cap) {
     R.alive = false;
   } else {
     R.t += P.tstep;
@@ -371,6 +367,16 @@ __device__ __forceinline__ bool group_any(bool b) {
   }
 }
 
+// The largest v over this lane's K-lane group (called by whole groups): acc = v to start.
+template <int K, int I = 0>
+__device__ __forceinline__ int group_max_i(int v, int acc) {
+  if constexpr (K == 1 || I == K) {
+    return acc;
+  } else {
+    return group_max_i<K, I + 1>(v, max(acc, __float_as_int(group_lane<K, I>(__int_as_float(v)))));
+  }
+}
+
 // Composite the existing samples (a prefix of the K; exf = 1 where this lane's sample exists) of a
 // depth-lane group in order, every lane of the group alike; the ray stops at the first sum.a > thr
 // (volumeRender_kernel.cu:482).
@@ -383,7 +389,7 @@ __device__ __forceinline__ bool group_any(bool b) {
 #endif
 template <int K, int I, bool ZF = false>
 __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, float exf, float r, float gg, float b,
-                                                float alpha) {
+                                                float alpha, float thr) {
   if constexpr (I < K) {
     const float ri = group_lane<K, I>(r), gi = group_lane<K, I>(gg), bi = group_lane<K, I>(b),
                 ai = group_lane<K, I>(alpha);
@@ -394,9 +400,9 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
       R.sg = fmaf(om, gi, R.sg);
       R.sb = fmaf(om, bi, R.sb);
       R.sa = fmaf(om, ai, R.sa);
-      if (R.sa > P.thr) R.alive = false;
+      if (R.sa > thr) R.alive = false;
     }
-    composite_group<K, I + 1, ZF>(P, R, exf, r, gg, b, alpha);
+    composite_group<K, I + 1, ZF>(P, R, exf, r, gg, b, alpha, thr);
   }
 }
 
@@ -421,11 +427,28 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // has the position, t and step count of the one-volume march.  A ray stops here when it
 // terminates, or at its first sample beyond the slab in its direction of travel (`past`), whose
 // state becomes the resume point (store_resume).
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
+// SPLIT (chord split, RenderParams::split_*): SR says the wave's role -- 0 the whole chord, 1 (A)
+// the samples below SR.n_split only, 2 (B) the samples from SR.n_split on, each stored to the ray's
+// records (SR.rec, compacted: the samples of empty-chunk leaps add exactly nothing and are not
+// stored) and composited locally only for B's own stop (opacity past P.split_thr); SR.wrote
+// returns the records this lane stored up to (B).
+struct SplitRole {
+  int role, n_split;
+  float *rec;  // this lane's ray's records (4 floats each)
+  int wrote;
+};
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false,
+          bool SPLIT = false>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
-                                      uint32_t kk = 0) {
+                                      uint32_t kk = 0, SplitRole *SR = nullptr) {
   static_assert(!COUNT || K == 1 || VR_COUNT_K, "the counter variant is built for K = 1 only (VR_COUNT_K: all K)");
   static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
+  static_assert(!SPLIT || (!SLAB && !COUNT), "chord split: not with slabs or counters");
+  // (wave-uniform) the sample cap and the exit threshold of this wave's role
+  const bool role_b = SPLIT && SR->role == 2;
+  const int cap = (SPLIT && SR->role == 1) ? min(SR->n_split, P.max_steps) : P.max_steps;
+  const float thr = role_b ? P.split_thr : P.thr;
+  int nrec = 0;  // B, K = 1: records stored (the compacted index of the next one)
   const float sbz = P.bmin[2], ssz = P.bscale[2];
   // slab mode: the ray has left the slab in its direction of travel (normalized z of its sample)
   auto beyond = [&](float zn) { return R.step.z >= 0.f ? zn >= P.slab_z1 : zn < P.slab_z0; };
@@ -433,9 +456,15 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   const int sub = lane & (K - 1);
   if constexpr (K > 1) {  // R.nsteps: 0, or the resume point's index (slab mode)
     R.mine = R.alive;
-    leap(P, sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to this lane's first sample
+    if (role_b)  // B: the recurrences of the first n_split samples replayed (exact), then this lane's
+      advance(P, SR->n_split + sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+    else
+      leap(P, sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // to this lane's first sample
     R.alive = group_any<K>(R.mine);
+  } else if (role_b) {
+    advance(P, SR->n_split, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
   }
+  int kb = 0;  // B, K > 1: compacted record index of this group's next iteration
 
   // VR_ADAPTIVE_S: the first box attempt of a chunk is twice the length the wave's last chunk
   // staged (its box grows little from one chunk to the next), and the shortest after a partial box,
@@ -500,12 +529,12 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     if (empty) {
       // tame waves: one exit test after the S additions (advance_n; t only grows)
       if constexpr (K == 1) {
-        if (COUNT || !VR_BRANCHFREE_LEAP) leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);  // exact counts
-        else if constexpr (!NANCHK) advance_n(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
-        else advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        if (COUNT || !VR_BRANCHFREE_LEAP) leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // exact counts
+        else if constexpr (!NANCHK) advance_n(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+        else advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
       } else {
-        if constexpr (!NANCHK) advance_n(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
-        else advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+        if constexpr (!NANCHK) advance_n(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+        else advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
         R.alive = R.alive && group_any<K>(R.mine);
       }
       continue;
@@ -542,7 +571,11 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
           R.nlit += shaded ? 1 : 0;
         }
-        composite(P, R, r, gg, b, alpha);
+        if (role_b) {  // B: the sample's record, in sample order (past the capacity: -2, reported)
+          if (nrec < (int)P.split_cap) *reinterpret_cast<float4 *>(SR->rec + 4 * nrec) = make_float4(r, gg, b, alpha);
+          SR->wrote = ++nrec;
+        }
+        composite(P, R, r, gg, b, alpha, thr, cap);
       }
     } else {
       // WC: the chunk's box is whole (sample_at skips its slot test); a separate copy of the loop,
@@ -569,7 +602,15 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           ++C.iter;
           C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
         }
-        composite_group<K, 0, VR_ZERO_FILL && !NANCHK && !SLAB>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha);
+        if (role_b) {  // B: the group's existing samples (a prefix of its K) as records kb + sub
+          if (ex) {
+            if (kb + sub < (int)P.split_cap)
+              *reinterpret_cast<float4 *>(SR->rec + 4 * (kb + sub)) = make_float4(r, gg, b, alpha);
+            SR->wrote = kb + sub + 1;
+          }
+          kb += K;
+        }
+        composite_group<K, 0, VR_ZERO_FILL && !NANCHK && !SLAB>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha, thr);
         if (SLAB && !inside) {
           if (R.alive && group_any<K>(R.mine && !ex)) {  // left the slab still unfinished
             // the next slab resumes at the group's first sample beyond this one (samples of a
@@ -584,9 +625,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           }
         }
         if constexpr (!NANCHK && !SLAB)  // tame: t is non-decreasing (tstep > 0), one test after K steps
-          advance_k<K>(P, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
+          advance_k<K>(P, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
         else
-          advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);  // to sample + K
+          advance(P, K, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // to sample + K
         R.alive = R.alive && group_any<K>(R.mine);
       }
       };
@@ -655,6 +696,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n, int run) {
 // rounds; uncapped registers, its longest waves share a SIMD with few others); 2: a full frame
 // (the occupancy cap of the unscheduled kernel); 3: a full frame following the order without
 // recording durations.
+// SCHED 4: a full frame in row-major order with the chord split of RenderParams::split_* (the
+// first split_n workgroups are the split blocks' back halves; split_composite_kernel follows).
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
@@ -662,11 +705,27 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
   constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
+  constexpr bool SPLIT = SCHED == 4;
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
-  uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
-  if (!SCHED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
-    wgo += P.block_rot;
-    if (wgo >= gridDim.x) wgo -= gridDim.x;
+  SplitRole SR{0, 0, nullptr, 0};
+  int slot = -1;
+  uint32_t wgo;
+  if constexpr (SPLIT) {
+    if (blockIdx.x < P.split_n) {  // a back half (B)
+      slot = (int)blockIdx.x;
+      wgo = P.split_list[slot];
+      SR.role = 2;
+    } else {
+      wgo = blockIdx.x - P.split_n;
+      slot = P.split_of[wgo];
+      SR.role = slot >= 0 ? 1 : 0;
+    }
+  } else {
+    wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
+    if (!SCHED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
+      wgo += P.block_rot;
+      if (wgo >= gridDim.x) wgo -= gridDim.x;
+    }
   }
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
   if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
@@ -701,19 +760,48 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
     R.t = tnear;
   }
-  // every coordinate the march forms from a finite start and step is finite; a tame launch takes
-  // the fast path (sample_at: TAME)
-  if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
-  else
-    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
+  // chord split: n_split = half the longest chord of the wave's rays in samples (wave-uniform; the
+  // same in the block's two halves, which set up the same rays); this lane's ray's records
+  const size_t rslot = SPLIT ? ((size_t)(slot * VR_WG_WAVES + wave) * (64 / K) + (size_t)ray) : 0;
+  if (SPLIT && SR.role) {
+    const int est = R.alive ? (int)fminf((R.tfar - R.t) / P.tstep, 1.0e9f) : 0;
+    SR.n_split = wave_max(est) >> 1;
+    SR.rec = P.split_rec + rslot * (size_t)P.split_cap * 4u;
+    if (SR.n_split < 1) {  // nothing to split in this wave: A marches it whole, B stores nothing
+      if (SR.role == 2) R.alive = false;
+      SR.role = SR.role == 1 ? 0 : 2;
+    }
+  }
+  if constexpr (SPLIT) {
+    if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP, false, true>(P, L, lane, R, C, 0u, &SR);
+    else
+      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP, false, true>(P, L, lane, R, C, 0u, &SR);
+  } else {
+    // every coordinate the march forms from a finite start and step is finite; a tame launch takes
+    // the fast path (sample_at: TAME)
+    if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
+    else
+      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
+  }
 
-  if (active && (lane & (K - 1)) == 0) {
+  if (SPLIT && SR.role == 2) {
+    // B: how many records this ray's lanes stored (the group's largest), and its pixel
+    const int n = group_max_i<K>(SR.wrote, SR.wrote);
+    if ((lane & (K - 1)) == 0) {
+      P.split_cnt[rslot] = active ? (n <= (int)P.split_cap ? n : -2) : -1;
+      P.split_pix[rslot] = active ? (uint32_t)((size_t)lc * (size_t)P.height + (size_t)y) : 0xffffffffu;
+    }
+  } else if (active && (lane & (K - 1)) == 0) {
     const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
     const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
     out[kk] = R.sr;
     out[kk + plane] = R.sg;
     out[kk + 2 * plane] = R.sb;
+    // A: the opacity to continue from when the ray did not stop (the reference goes on while
+    // !(sum.a > thr)); -1: stopped, nothing to add
+    if (SPLIT && slot >= 0) P.split_hand[rslot] = (SR.role == 1 && !(R.sa > P.thr)) ? R.sa : -1.f;
   }
   if (TIMED) {  // this block's duration, for the next launch's schedule
     __syncthreads();
@@ -1004,6 +1092,10 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   // scheduled kernels: K > 1, fast variant only (otherwise the names below alias the SCHED 0 kernel)
   constexpr bool SCH = K > 1 && VR_MARCH_FAST;
   constexpr int S1 = SCH ? 1 : 0, S2 = SCH ? 2 : 0, S3 = SCH ? 3 : 0;
+  // the chord-split kernel (SCHED 4) only where the host splits: lit, absorption = emission, the
+  // default slot (vr_capi.hip split_plan)
+  constexpr bool SPL = SCH && AB && MODE >= 1 && CAP == VR_LDS_CAP;
+  constexpr int S4 = SPL ? 4 : 0;
 #define VR_LAUNCH(KK, CNT, BG, SC, PAD)                                                                    \
   do {                                                                                                    \
     hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, PAD, s, P);        \
@@ -1017,6 +1109,9 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
     else VR_LAUNCH(K, VR_COUNT_K != 0, false, 0, 0);
   } else if (!VR_MARCH_FAST && sched) {  // the exact variant is built without the scheduled kernels
     return hipErrorInvalidValue;
+  } else if (P.split_n) {  // a full frame with its heaviest blocks split (not scheduled, 32-bit)
+    if (!SPL || big || sched) return hipErrorInvalidValue;
+    VR_LAUNCH(K, false, false, S4, 0);
   } else if (K > 1 && sched && P.sched_full == 1) {  // a full frame, durations measured
     if (big) VR_LAUNCH(K, false, true, S2, 0);
     else VR_LAUNCH(K, false, false, S2, 0);
@@ -1063,7 +1158,8 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
   if (P.views > 1 && (P.view_blocks != per_view || !P.out2)) return hipErrorInvalidValue;
-  const dim3 grid(per_view * (P.views > 1 ? 2u : 1u));
+  if (P.split_n && (P.views > 1 || !P.split_list || !P.split_of || VR_MARCH_K == 1)) return hipErrorInvalidValue;
+  const dim3 grid(per_view * (P.views > 1 ? 2u : 1u) + P.split_n);  // (split: the back halves first)
   if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || VR_MARCH_K == 1))
     return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {

@@ -456,7 +456,12 @@ __device__ __forceinline__ float divpi(float x) {
 #define VR_FAST_GXQ 0  // 1: gamma's cosine as dot / (v_sqrt(lip.lip) v_sqrt(lop.lop)), one-correction quotient
 #endif
 #ifndef VR_FAST_HYBQ
-#define VR_FAST_HYBQ 0  // 1: gamma's cosine correctly rounded (the oracle's) only in waves with |cos| > VR_HYB_TG
+// gamma's cosine as the oracle's correctly rounded quotient where |cos gamma| > VR_HYB_TG: 2 (the
+// default since round 4) per lane with the compiler's IEEE sequences; 1 per wave with the guarded
+// sequences (measured slower); 0 never.  Near |cos| = 1 acos amplifies the rsq cosine's rounding
+// into the 8-bit LUT weight: this is what held the fast shading at 99.90-99.92 % of the SURVEY
+// tolerance; with it 99.97-99.98 %, at +5 % of the metric kernel.
+#define VR_FAST_HYBQ 2
 #endif
 #ifndef VR_FAST_HYBRID
 #define VR_FAST_HYBRID 0  // 1: rsq shading, and XN + XG shading where gamma is ill-conditioned (shade_fast)
@@ -465,7 +470,8 @@ __device__ __forceinline__ float divpi(float x) {
 #define VR_HYB_TA 0.01f  // hybrid: |lip|^2 < TA |li|^2 (view within asin(0.1) of the normal), same for lights
 #endif
 #ifndef VR_HYB_TG
-#define VR_HYB_TG 0.995f  // hybrid: |cos gamma| > TG
+#define VR_HYB_TG 0.999f  // |cos gamma| > TG: the oracle's quotient (VR_FAST_HYBQ; below gamma = 0.0245 the
+                          // LUT taps clamp to one voxel and the weight no longer matters)
 #endif
 #ifndef VR_RSQ_NR
 #define VR_RSQ_NR 0  // 1: one Newton step on every cosine's hardware rsq
@@ -641,7 +647,11 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     else if (VR_FAST_GXQ) q = div_short(dot3(lip, lop), rlip * __builtin_amdgcn_sqrtf(lop2));
     else q = dot3(lip, lop) * (rlip * rsq_c(lop2));
     if constexpr (NEED) need = need || fabsf(q) > VR_HYB_TG || lop2 < VR_HYB_TA * dot3(lo, lo);
-    if constexpr (VR_FAST_HYBQ && !XG && !NEED) {
+    if constexpr (VR_FAST_HYBQ == 2 && !XG && !NEED) {
+      // per lane, no wave-wide guard: near |cos| = 1 (where acos amplifies the cosine's rounding) the
+      // oracle's quotient dot / (sqrtf(lip.lip) sqrtf(lop.lop)) with the compiler's IEEE sequences
+      if (__builtin_expect(fabsf(q) > VR_HYB_TG, 0)) q = dot3(lip, lop) / (sqrtf(lip2) * sqrtf(lop2));
+    } else if constexpr (VR_FAST_HYBQ == 1 && !XG && !NEED) {
       // near |cos| = 1 acos amplifies the cosine's rounding: there the oracle's quotient
       const bool nd = fabsf(q) > VR_HYB_TG;
       if (__builtin_expect(__any(nd), 0)) {

@@ -170,33 +170,6 @@ __device__ __forceinline__ f3 half_grad_lds(const float *L, const Box &B, int ac
   return g;
 }
 
-// The lookup gradient of a sample whose three gradient volumes are MATLAB's gradient of the
-// emission volume (RenderParams::gderived; Volume.m:181-205 -> gradient(Data)): each corner value
-// of the lookups' 2x2x2 cell is the central difference (f(c + 1) - f(c - 1)) / 2 the gradient volume
-// holds at an interior voxel, taken from the staged emission voxels, and the corners are interpolated
-// exactly as fetch_vec interpolates the stored values (lerp x, then y, then z, per component) --
-// bit-identical to the gather for a cell whose corners are all interior (1 <= c <= n - 2 on every
-// axis: the one-sided ends are not derived here).  MATLAB's gx is the derivative along array
-// dimension 2 (slot rows, pitch px), gy along dimension 1 (slot x), gz along dimension 3 (planes).
-// The slot must hold voxels i - 1 .. i + 2 on every axis (the host's staging halo: tap_off >= 1).
-__device__ __forceinline__ f3 cd_grad_lds(const float *L, const Box &B, int ac, float wx, float wy, float wz) {
-  const int px = B.px, pxy = B.pxy;
-  // central difference along the axis of pitch s at slot word a (single precision, as MATLAB's)
-  auto cd = [&](int a, int s) { return (L[a + s] - L[a - s]) / 2.f; };
-  auto tri = [&](int s) {
-    const float c00 = lerp(cd(ac, s), cd(ac + 1, s), wx);
-    const float c10 = lerp(cd(ac + px, s), cd(ac + px + 1, s), wx);
-    const float c01 = lerp(cd(ac + pxy, s), cd(ac + pxy + 1, s), wx);
-    const float c11 = lerp(cd(ac + pxy + px, s), cd(ac + pxy + px + 1, s), wx);
-    return lerp(lerp(c00, c10, wy), lerp(c01, c11, wy), wz);
-  };
-  f3 g;
-  g.x = tri(px);
-  g.y = tri(1);
-  g.z = tri(pxy);
-  return g;
-}
-
 // Slot coordinates of a tap pair base and whether the cell [l, l+1] lies in the box along it.
 __device__ __forceinline__ int slot_coord(int i, int r) { return (int)((uint32_t)i + 1u - (uint32_t)r); }
 __device__ __forceinline__ bool in_box(int l, int e) {
@@ -455,11 +428,14 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
 // The empty-chunk leap: every tap of the chunk lies in the staged all-zero box, so each sample has
 // em = ab = 0, alpha = 1 - exp(-0) = 0 and adds exactly 0 (skip_empty proves the shading term
 // finite).  Only the march recurrences run, in the reference's order.
+// cap (all four): the sample-count cap, P.max_steps unless given (a chord split's front half, A,
+// stops at its split index: vr_march.hip SPLIT)
 __device__ __forceinline__ void leap(const RenderParams &P, int S, bool &alive, int32_t &nsteps, float &t,
-                                     float tfar, f3 &pos, const f3 &step) {
+                                     float tfar, f3 &pos, const f3 &step, int cap = -1) {
+  const int mx = cap < 0 ? P.max_steps : cap;
   for (int k = 0; k < S && alive; ++k) {
     ++nsteps;
-    if (nsteps >= P.max_steps) {
+    if (nsteps >= mx) {
       alive = false;
     } else {
       t += P.tstep;
@@ -473,25 +449,26 @@ __device__ __forceinline__ void leap(const RenderParams &P, int S, bool &alive, 
 // stopped existing keeps advancing, but its state is never read again (`alive` stays false), so
 // the live lanes see exactly leap()'s additions.
 __device__ __forceinline__ void advance(const RenderParams &P, int n, bool &alive, int32_t &nsteps, float &t,
-                                        float tfar, f3 &pos, const f3 &step) {
+                                        float tfar, f3 &pos, const f3 &step, int cap = -1) {
+  const int mx = cap < 0 ? P.max_steps : cap;
   for (int k = 0; k < n; ++k) {
     ++nsteps;
     t += P.tstep;
     pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
-    alive = alive && nsteps < P.max_steps && !(t > tfar);
+    alive = alive && nsteps < mx && !(t > tfar);
   }
 }
 
 // advance() for a tame launch (tstep > 0, finite): the additions of n samples, then one exit test
 // (t only grows and nsteps only counts up, so the intermediate tests are implied by the last).
 __device__ __forceinline__ void advance_n(const RenderParams &P, int n, bool &alive, int32_t &nsteps, float &t,
-                                          float tfar, f3 &pos, const f3 &step) {
+                                          float tfar, f3 &pos, const f3 &step, int cap = -1) {
   for (int k = 0; k < n; ++k) {
     t += P.tstep;
     pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
   }
   nsteps += n;
-  alive = alive && nsteps < P.max_steps && !(t > tfar);
+  alive = alive && nsteps < (cap < 0 ? P.max_steps : cap) && !(t > tfar);
 }
 
 // advance() by a compile-time count for a tame launch (tstep > 0, finite): t only grows and nsteps
@@ -499,14 +476,14 @@ __device__ __forceinline__ void advance_n(const RenderParams &P, int n, bool &al
 // the same `alive`, with the same rounded additions, and one test instead of n.
 template <int N>
 __device__ __forceinline__ void advance_k(const RenderParams &P, bool &alive, int32_t &nsteps, float &t, float tfar,
-                                          f3 &pos, const f3 &step) {
+                                          f3 &pos, const f3 &step, int cap = -1) {
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     t += P.tstep;
     pos = mk(pos.x + step.x, pos.y + step.y, pos.z + step.z);
   }
   nsteps += N;
-  alive = alive && nsteps < P.max_steps && !(t > tfar);
+  alive = alive && nsteps < (cap < 0 ? P.max_steps : cap) && !(t > tfar);
 }
 
 }  // namespace vr

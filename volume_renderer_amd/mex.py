@@ -222,12 +222,6 @@ def render_device(handle, ra: VrRenderArgs, d_out: int, part=None, d_steps: int 
                                  ctypes.c_void_p(int(stream)) if stream else None))
 
 
-def last_march_flags() -> int:
-    """Launch options of the last march launch (bit 1: lookup gradient derived from the staged
-    emission voxels)."""
-    return int(lib().vr_last_march_flags())
-
-
 def last_march_kernel() -> str:
     """The demangled name of the march kernel instantiation the last render launched."""
     buf = ctypes.create_string_buffer(256)
