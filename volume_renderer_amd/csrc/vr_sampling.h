@@ -456,12 +456,11 @@ __device__ __forceinline__ float divpi(float x) {
 #define VR_FAST_GXQ 0  // 1: gamma's cosine as dot / (v_sqrt(lip.lip) v_sqrt(lop.lop)), one-correction quotient
 #endif
 #ifndef VR_FAST_HYBQ
-// gamma's cosine as the oracle's correctly rounded quotient where |cos gamma| > VR_HYB_TG: 2 (the
-// default since round 4) per lane with the compiler's IEEE sequences; 1 per wave with the guarded
-// sequences (measured slower); 0 never.  Near |cos| = 1 acos amplifies the rsq cosine's rounding
-// into the 8-bit LUT weight: this is what held the fast shading at 99.90-99.92 % of the SURVEY
-// tolerance; with it 99.97-99.98 %, at +5 % of the metric kernel.
-#define VR_FAST_HYBQ 2
+// gamma's cosine as the oracle's correctly rounded quotient where |cos gamma| > VR_HYB_TG (parity
+// ablation, round 4): 2 per lane with the compiler's IEEE sequences, 1 per wave with the guarded
+// sequences, 0 never (default: VR_FAST_CLAMP takes care of what they fixed, at a fraction of their
+// +5 % cost).
+#define VR_FAST_HYBQ 0
 #endif
 #ifndef VR_FAST_HYBRID
 #define VR_FAST_HYBRID 0  // 1: rsq shading, and XN + XG shading where gamma is ill-conditioned (shade_fast)
@@ -472,6 +471,11 @@ __device__ __forceinline__ float divpi(float x) {
 #ifndef VR_HYB_TG
 #define VR_HYB_TG 0.999f  // |cos gamma| > TG: the oracle's quotient (VR_FAST_HYBQ; below gamma = 0.0245 the
                           // LUT taps clamp to one voxel and the weight no longer matters)
+#endif
+#ifndef VR_HYB_TU
+// ... and |cos gamma| < TU: beyond it gamma is within 0.0245 of 0 or pi, where both taps of the LUT's
+// gamma axis are the same voxel (the weight does not matter); 2: no upper bound
+#define VR_HYB_TU 2.f
 #endif
 #ifndef VR_RSQ_NR
 #define VR_RSQ_NR 0  // 1: one Newton step on every cosine's hardware rsq
@@ -499,6 +503,24 @@ __device__ __forceinline__ float rcp_sqrt_cr(float x) {
   return 1.f / sqrtf(x);
 }
 extern "C" __device__ float __ocml_acospi_f32(float);
+__device__ __forceinline__ float acospi_q(float q);
+// acos(q) / pi of a fast-shading cosine (shade_fast).  VR_FAST_CLAMP (default 1, inside acospi_q at
+// no cost; 2: an explicit compare and select here): a cosine the rsq product rounds below -1 is
+// taken as -1, NaN kept.  Where the exact cosine lies within a few ulps
+// of -1 (a back-facing normal, a light opposite the view in the tangent plane) the rsq product and
+// the oracle's correctly rounded quotient round past -1 independently, and past it acosf is NaN,
+// which the LUT lookup reads as the coordinate 0 -- the LUT at angle 0 instead of pi.  The fp64
+// oracle never rounds past; taking the cosine as -1 agrees with it everywhere and with the fp32
+// oracle wherever that one does not round past either (where it does, the envelope |fp32 - fp64|
+// holds the difference).  Past +1 needs no care: angle 0 and the NaN's coordinate 0 read the same
+// LUT voxels.  This was the whole of the fast shading's remaining SURVEY 8c gap.
+#ifndef VR_FAST_CLAMP
+#define VR_FAST_CLAMP 1
+#endif
+__device__ __forceinline__ float acospi_f(float q) {
+  if (VR_FAST_CLAMP == 2) q = q < -1.f ? -1.f : q;  // (the explicit form: a compare and a select)
+  return acospi_q(q);
+}
 __device__ __forceinline__ float acospi_q(float q) {
 #if VR_ABLATE & 2
   return fmaf(q, -0.5f, 0.5f);  // diagnostic: the angle's cost removed (wrong image)
@@ -533,7 +555,10 @@ __device__ __forceinline__ float acospi_q(float q) {
   p = fmaf(p, t, -6.830968708e-02f);
   p = fmaf(p, t, 0.5f);
 #endif
-  const float r = __builtin_amdgcn_sqrtf(1.f - t) * p;
+  // VR_FAST_CLAMP 1: sqrt(|1 - t|) -- a free source modifier -- is the clamp of acospi_f for the few
+  // ulps a rounded cosine can exceed 1 in magnitude (the result within sqrt(ulp) of 0 or 1, in the
+  // LUT's clamped end cell either way) and keeps NaN; with 1 - t alone they are NaN (coordinate 0)
+  const float r = __builtin_amdgcn_sqrtf(VR_FAST_CLAMP == 1 ? fabsf(1.f - t) : 1.f - t) * p;
   // q < 0 ? 1 - r : r without a compare: fma(-1, r, 1) rounds as 1 - r, fma(1, r, 0) is r (q = -0
   // takes the first form: 1 - 0.5 = 0.5 = r, the same value)
   const float sg = __builtin_copysignf(1.f, q);
@@ -650,7 +675,8 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     if constexpr (VR_FAST_HYBQ == 2 && !XG && !NEED) {
       // per lane, no wave-wide guard: near |cos| = 1 (where acos amplifies the cosine's rounding) the
       // oracle's quotient dot / (sqrtf(lip.lip) sqrtf(lop.lop)) with the compiler's IEEE sequences
-      if (__builtin_expect(fabsf(q) > VR_HYB_TG, 0)) q = dot3(lip, lop) / (sqrtf(lip2) * sqrtf(lop2));
+      const float aq = fabsf(q);
+      if (__builtin_expect(aq > VR_HYB_TG && aq < VR_HYB_TU, 0)) q = dot3(lip, lop) / (sqrtf(lip2) * sqrtf(lop2));
     } else if constexpr (VR_FAST_HYBQ == 1 && !XG && !NEED) {
       // near |cos| = 1 acos amplifies the cosine's rounding: there the oracle's quotient
       const bool nd = fabsf(q) > VR_HYB_TG;
@@ -662,7 +688,7 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     return q;
   };
   if constexpr (NEED) need = lip2 < VR_HYB_TA * li2;
-  const float alpha_n = acospi_q(dot3(n, li) * (rn * rsq_c(li2)));
+  const float alpha_n = acospi_f(dot3(n, li) * (rn * rsq_c(li2)));
   const AxF la = axis_lut<true>(alpha_n, P.lut.fnx);
   int i = 0;
   if (TAME || (P.lut.p != nullptr && P.lut.small && !P.lut.one)) {
@@ -675,10 +701,10 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
       const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
       const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
       const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-      const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
-      const float gamma0 = acospi_q(gamma_q(lo0, lop0));
-      const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
-      const float gamma1 = acospi_q(gamma_q(lo1, lop1));
+      const float beta0 = acospi_f(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
+      const float gamma0 = acospi_f(gamma_q(lo0, lop0));
+      const float beta1 = acospi_f(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
+      const float gamma1 = acospi_f(gamma_q(lo1, lop1));
       float light0, light1;
 #if VR_ABLATE & 1  // diagnostic: the LUT fetch's cost removed (wrong image)
       light0 = beta0 + gamma0 + la.w;
@@ -708,10 +734,10 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
     const f3 lop0 = mk(fmaf(-dlo0, n.x, lo0.x), fmaf(-dlo0, n.y, lo0.y), fmaf(-dlo0, n.z, lo0.z));
     const f3 lop1 = mk(fmaf(-dlo1, n.x, lo1.x), fmaf(-dlo1, n.y, lo1.y), fmaf(-dlo1, n.z, lo1.z));
-    const float beta0 = acospi_q(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
-    const float gamma0 = acospi_q(gamma_q(lo0, lop0));
-    const float beta1 = acospi_q(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
-    const float gamma1 = acospi_q(gamma_q(lo1, lop1));
+    const float beta0 = acospi_f(dlo0 * (rn * rsq_c(dot3(lo0, lo0))));
+    const float gamma0 = acospi_f(gamma_q(lo0, lop0));
+    const float beta1 = acospi_f(dlo1 * (rn * rsq_c(dot3(lo1, lo1))));
+    const float gamma1 = acospi_f(gamma_q(lo1, lop1));
     const float light0 = lut_light<true>(P.lut, la, beta0, gamma0);
     const float light1 = lut_light<true>(P.lut, la, beta1, gamma1);
     const float rl0 = refl * light0;
@@ -728,8 +754,8 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
     const float dlo = dot3(lo, n);
     const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
-    const float beta = acospi_q(dlo * (rn * rsq_c(dot3(lo, lo))));
-    const float gamma = acospi_q(gamma_q(lo, lop));
+    const float beta = acospi_f(dlo * (rn * rsq_c(dot3(lo, lo))));
+    const float gamma = acospi_f(gamma_q(lo, lop));
     const float rl = refl * (TAME ? (VR_LUT_ZPAIR ? fetch_small_z(P.lut, la, axis_lut<true>(beta, P.lut.fny),
                                                                  axis_lut<true>(gamma, P.lut.fnz))
                                                   : fetch_small(P.lut, la, axis_lut<true>(beta, P.lut.fny),
