@@ -75,7 +75,8 @@ hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
-hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s);
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, uint64_t pxy,
+                              hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_split_composite(const RenderParams &P, uint32_t nrays, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
@@ -1310,7 +1311,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   // the oracle's correctly rounded op sequence (bit-identical to oracle/vr_oracle.c up to acosf)
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
   if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
-  P.xcd_run = VR_XCD_RUN;
+  // XCD runs of 16 blocks for lookup-gradient frames (their gathers of the gradient copy are the
+  // launch's HBM traffic: C3 36.4 -> 35.7 ms, round 4); the compute-gradient march is indifferent
+  P.xcd_run = F.mode == 2 ? 16 : VR_XCD_RUN;
   if (const char *ev = std::getenv("VR_XCD_RUN")) P.xcd_run = std::max(0, std::atoi(ev));  // A/B switch
   P.block_rot = 0;  // set at the launch (block rows of the launch's depth lanes)
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
@@ -1343,11 +1346,12 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const uint64_t n = bx->bytes / sizeof(float);
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
-      gv->bytes = n * 4 * sizeof(float);
+      gv->bytes = n * (VR_GVEC_ZPAIR ? 8 : 4) * sizeof(float);
       const hipError_t ea = vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device);
       if (ea == hipSuccess) {
         for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);
-        VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
+        const uint64_t pxy = (bx->dims[0] + 2) * (bx->dims[1] + 2);
+        VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, pxy, stream));
         // launches on other streams (another handle, a group's other children on this device) find
         // the copy fresh and wait for this event before reading it (bind_reads)
         VR_HIP(vr_host::record_event(stream, gv->ready));

@@ -5,6 +5,14 @@
 
 namespace vr {
 
+// Layout of the interleaved lookup gradient (RenderParams::gvec).  0 (default): (gx, gy, gz, 0) per
+// padded voxel.  1 (A/B, round 4): z-paired -- entry i is 32 bytes, voxel i and voxel i + pxy (the
+// next plane), so a lookup's eight corners lie in two 64-byte runs instead of four 32-byte runs;
+// measured slower (C3 37.7 vs 36.4 ms: twice the footprint), DESIGN.md s8.
+#ifndef VR_GVEC_ZPAIR
+#define VR_GVEC_ZPAIR 0
+#endif
+
 // A bound "texture": an fp32 volume resident in HBM in the apron layout of DESIGN.md s5 -- the
 // logical nx*ny*nz column-major volume (x fastest) surrounded by a one-voxel border that
 // replicates the edge voxels, i.e. P[k][j][i] = T[clamp(k-1)][clamp(j-1)][clamp(i-1)] for
@@ -57,7 +65,7 @@ struct RenderParams {
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
-  const float *gvec;              // lookup gradient interleaved (gx,gy,gz,0) x padded voxels, or null
+  const float *gvec;              // lookup gradient interleaved (VR_GVEC_ZPAIR layout), or null
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test

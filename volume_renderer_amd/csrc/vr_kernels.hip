@@ -446,12 +446,31 @@ __global__ __launch_bounds__(256) void interleave3_kernel(const float *__restric
     out[i] = make_float4(a[i], b[i], c[i], 0.f);
 }
 
-hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, hipStream_t s) {
+// The z-paired interleave (VR_GVEC_ZPAIR): entry i = (a, b, c, 0) of voxel i, then of voxel i + pxy
+// (the last plane's second half repeats its first: no lookup reads it -- a cell's upper plane is at
+// most the apron plane, whose entries lie one plane below).
+__global__ __launch_bounds__(256) void interleave3z_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                           const float *__restrict__ c, float4 *__restrict__ out,
+                                                           uint64_t n, uint64_t pxy) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = i + pxy < n ? i + pxy : i;
+    out[2 * i] = make_float4(a[i], b[i], c[i], 0.f);
+    out[2 * i + 1] = make_float4(a[j], b[j], c[j], 0.f);
+  }
+}
+
+// out: n entries of the VR_GVEC_ZPAIR layout (pxy: the plane pitch of the padded volume)
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, uint64_t pxy,
+                              hipStream_t s) {
   if (!n) return hipSuccess;
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 262144) blocks = 262144;
-  hipLaunchKernelGGL(interleave3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
-                     reinterpret_cast<float4 *>(out), n);
+  if (VR_GVEC_ZPAIR)
+    hipLaunchKernelGGL(interleave3z_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
+                       reinterpret_cast<float4 *>(out), n, pxy);
+  else
+    hipLaunchKernelGGL(interleave3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
+                       reinterpret_cast<float4 *>(out), n);
   return hipGetLastError();
 }
 
