@@ -97,7 +97,9 @@ def main():
         kind, _, rest = st.partition(":")
         print(f"step {kind}: {rest[:120]}", flush=True)
         if kind == "tests":
-            cmd = [PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-v", "--timeout", "120",
+            # -rP: the captured output of passed tests too (the PARITY lines of test_full_size.py,
+            # tools/parity_summary.py)
+            cmd = [PY, "-u", "-m", "pytest", "tests", "-m", "gpu", "-x", "-v", "-rP", "--timeout", "120",
                    "--timeout-method", "thread"] + (["-k", rest] if rest else [])
             rc = run(cmd, os.path.join(out, "tests.log"), 900)
         elif kind == "ab":
