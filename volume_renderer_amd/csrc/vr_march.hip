@@ -659,7 +659,12 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 #ifndef VR_MARCH_MIN_EU
 #define VR_MARCH_MIN_EU 5
 #endif
-constexpr int march_min_eu(int cap, int sched) { return (cap <= VR_LDS_CAP && sched != 1) ? VR_MARCH_MIN_EU : 1; }
+#ifndef VR_SCHED1_MIN_EU
+#define VR_SCHED1_MIN_EU 1  // a short (scheduled) launch's occupancy cap (A/B; 1: uncapped registers)
+#endif
+constexpr int march_min_eu(int cap, int sched) {
+  return cap <= VR_LDS_CAP ? (sched != 1 ? VR_MARCH_MIN_EU : VR_SCHED1_MIN_EU) : 1;
+}
 #ifndef VR_WG_WAVES
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
 #endif
