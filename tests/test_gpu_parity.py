@@ -423,6 +423,36 @@ def test_chord_split_is_bit_identical(monkeypatch, counter_clock, scene, k):
     r.delete()
 
 
+def test_chord_split_in_partitions(monkeypatch, counter_clock):
+    """The chord split inside the image partition's part launches (each part its own launch of the
+    split kernel, as a rank would run it): the parts assemble to the unsplit full frame bit for bit."""
+    import torch
+    from volume_renderer_amd import mex
+    v = vr.Volume(O.shell_volume(48))
+    r = ex1_renderer(v, res=(131, 93))
+    monkeypatch.setenv("VR_DEPTH_LANES", "4")
+    full = r.render()
+    args = (r.LightSources, r.VolumeIllumination,
+            np.float32([r.FactorEmission, r.FactorReflection, r.FactorAbsorption]), np.float32(r.ElementSizeUm),
+            np.uint64([93, 131]), np.flip(r.RotationMatrix, 0).astype(np.float32),
+            np.float32([0, r.FocalLength, r.DistanceToObject]), np.float32(r.OpacityThreshold), np.float32(r.Color))
+    ra, keep = mex.render_args(*args)
+    W, H = 131, 93
+    monkeypatch.setenv("VR_SPLIT_FORCE", "0.5")
+    for nparts, bc in ((2, 16), (4, 8)):
+        maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
+        parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
+        for p in range(nparts):
+            mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts))
+            assert mex.last_march_kernel().endswith(", 4>"), mex.last_march_kernel()
+        out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
+        mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
+        torch.cuda.synchronize()
+        img = out.cpu().numpy().reshape(-1)
+        assert np.array_equal(img.view(np.uint32), full.reshape(-1, order="F").view(np.uint32)), (nparts, bc)
+    r.delete()
+
+
 @pytest.mark.parametrize("edge", [64, 128])
 def test_half_texel_taps(monkeypatch, counter_clock, edge):
     """Fast variant on a power-of-two cube (vr_capi.hip half_texel_taps): the on-the-fly gradient

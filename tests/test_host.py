@@ -240,6 +240,21 @@ def test_committed_traffic_matches_bench_default_workload():
         assert e["bytes_per_launch"] > 0 and e["kernel"].startswith("vr::fast::march_kernel<")
 
 
+def test_binding_roof_names_the_largest_hardware_fraction():
+    """bench.py roofline.binding: the largest of the fetched-bytes, counter-traffic and VALU
+    fractions (the F-weighted sample-stream fraction is not a candidate)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    rf = {"frac": 1.07, "fetched": {"frac": 0.46}, "traffic": 1.0e12, "valu": {"frac": 0.62}}
+    b = bench.binding_roof(rf, 0.265)  # 1 TB in 265 ms = 3.77 TB/s = 0.47 of 8 TB/s
+    assert b["roof"] == "valu" and b["frac"] == 0.62
+    assert abs(b["candidates"]["hbm_traffic"] - 1.0e12 / 0.265 / 8e12) < 1e-3
+    b = bench.binding_roof({"frac": 0.9, "fetched": {"frac": 0.23}, "traffic": 1.05e11, "valu": None}, 0.017)
+    assert b["roof"] == "hbm_traffic" and set(b["candidates"]) == {"fetched", "hbm_traffic"}
+    assert bench.binding_roof({"frac": 0.9, "fetched": {"frac": 0.4}, "traffic": None, "valu": None}, 0.03)["roof"] == "fetched"
+
+
 def test_cpu_share_is_positive():
     import sys
     sys.path.insert(0, ROOT)
