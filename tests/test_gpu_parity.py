@@ -453,6 +453,49 @@ def test_chord_split_in_partitions(monkeypatch, counter_clock):
     r.delete()
 
 
+@pytest.mark.parametrize("scene", ["hg2", "lookup", "dense"])
+def test_short_launch_split_is_bit_identical(monkeypatch, counter_clock, scene):
+    """The in-workgroup chord split of a short launch (VR_SPLIT_SHORT=1, vr_march.hip SCHED 5): from
+    the second launch of a part on, its heaviest blocks (by the previous launch's durations) are
+    marched by two workgroups whose wave pairs take each tile's front and back halves, the back half's
+    samples composited in order by the front wave after a workgroup barrier.  Every launch of every
+    part assembles to the unsplit frame bit for bit, at every split threshold."""
+    import torch
+    from volume_renderer_amd import mex
+    data = O.shell_volume(64)
+    if scene == "dense":
+        data = np.asfortranarray(data * 2 + 0.02, dtype=np.float32)
+    v = vr.Volume(data)
+    r = ex1_renderer(v, res=(149, 101))
+    if scene == "lookup":
+        r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
+    full = r.render()
+    args = (r.LightSources, r.VolumeIllumination,
+            np.float32([r.FactorEmission, r.FactorReflection, r.FactorAbsorption]), np.float32(r.ElementSizeUm),
+            np.uint64([101, 149]), np.flip(r.RotationMatrix, 0).astype(np.float32),
+            np.float32([0, r.FocalLength, r.DistanceToObject]), np.float32(r.OpacityThreshold), np.float32(r.Color))
+    ra, keep = mex.render_args(*args)
+    W, H = 149, 101
+    monkeypatch.setenv("VR_SPLIT_SHORT", "1")
+    for num in ("6", "1"):
+        monkeypatch.setenv("VR_SPLIT_SHORT_NUM", num)
+        for nparts, bc in ((2, 16), (4, 8)):
+            maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
+            for launch in range(3):
+                parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
+                for p in range(nparts):
+                    mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts))
+                    name = mex.last_march_kernel()
+                    assert name.endswith(", 5>"), name
+                out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
+                mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
+                torch.cuda.synchronize()
+                img = out.cpu().numpy().reshape(-1)
+                assert np.array_equal(img.view(np.uint32), full.reshape(-1, order="F").view(np.uint32)), \
+                    (scene, num, nparts, launch)
+    r.delete()
+
+
 @pytest.mark.parametrize("edge", [64, 128])
 def test_half_texel_taps(monkeypatch, counter_clock, edge):
     """Fast variant on a power-of-two cube (vr_capi.hip half_texel_taps): the on-the-fly gradient

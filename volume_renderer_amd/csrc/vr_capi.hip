@@ -70,7 +70,7 @@ VR_DECL_MARCH(fast)
 VR_DECL_MARCH(exact)
 #undef VR_DECL_MARCH
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s, uint32_t heavy_div,
-                        uint64_t tail);
+                        uint64_t tail, uint32_t *split_n = nullptr, uint32_t split_num = 0, uint32_t split_cap = 0);
 hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
@@ -262,6 +262,7 @@ struct vr_context {
     int32_t *d_split_cnt = nullptr;
     uint32_t *d_split_pix = nullptr;
     size_t split_rec_bytes = 0;
+    uint32_t *d_split_count = nullptr;  // short launches (SCHED 5): the order kernel's split count
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -616,6 +617,7 @@ struct Frame {
   bool degenerate = false;
   vr_context::Schedule *sched_copy = nullptr;  // a timed full-frame launch: copy its durations back
   vr_context::Schedule *sched = nullptr;       // the launch shape's schedule (attach_schedule)
+  bool split_short = false;  // a short launch may split its heaviest blocks in-workgroup (SCHED 5)
 };
 
 
@@ -946,6 +948,11 @@ bool want_schedule(const vr::RenderParams &P) {
 std::vector<uint32_t> split_choose(const uint32_t *cost, uint32_t nb, uint32_t W);
 hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uint32_t nb,
                         const std::vector<uint32_t> *chosen, hipStream_t stream);
+hipError_t split_records(vr_context::Schedule &S, const vr::RenderParams &P, uint32_t rays, hipStream_t stream);
+
+#ifndef VR_SPLIT_SHORT_NUM
+#define VR_SPLIT_SHORT_NUM 6  // in-workgroup split of a short launch: blocks >= 6/16 of the longest
+#endif
 
 // launch_order's tail argument: (tail_pct << 32) | resident workgroups; tail_pct 0 = heavy-first.
 uint64_t wg_tail_arg(uint32_t tail_pct) {
@@ -983,14 +990,34 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   const bool full = !short_launch(P) && !env_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
   if (!full) {  // short launch: every launch measured, ordered longest first by the previous one
     P.sched_full = 0;
+    // in-workgroup chord split (SCHED 5, F.split_short): the order kernel also counts the blocks to
+    // split (the leading ones lasting >= VR_SPLIT_SHORT_NUM / 16 of the longest, at most nb / 4)
+    uint32_t ns_cap = 0, num = VR_SPLIT_SHORT_NUM;
+    if (const char *ev = std::getenv("VR_SPLIT_SHORT_NUM")) num = (uint32_t)std::min(16, std::max(1, std::atoi(ev)));
+    if (F.split_short && nb >= 8) {
+      hipError_t e = S.d_split_count ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&S.d_split_count), sizeof(uint32_t));
+      if (e == hipSuccess) e = split_records(S, P, (nb / 4) * 4u * (64u / (uint32_t)K), stream);
+      if (e == hipSuccess) ns_cap = nb / 4;
+      else vr_host::consume(e, "split buffers (the short launch runs unsplit)");
+    }
     if (S.measured) {
       // VR_SCHED_SHORT_DIV=d (A/B): the heavy blocks (>= 1/d of the longest) first, the rest row-major
       uint32_t div = 0;
       if (const char *ev = std::getenv("VR_SCHED_SHORT_DIV")) div = (uint32_t)std::max(0, std::atoi(ev));
-      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, div, div ? wg_tail_arg(0) : 0u);
+      if (ns_cap) div = 0;
+      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, div, div ? wg_tail_arg(0) : 0u,
+                            ns_cap ? S.d_split_count : nullptr, num, ns_cap);
     } else {  // first launch of this shape: row-major order, durations recorded
       rc = vr::launch_iota(S.d_order, nb, stream);
+      if (rc == hipSuccess && ns_cap) rc = hipMemsetAsync(S.d_split_count, 0, sizeof(uint32_t), stream);
       S.measured = true;
+    }
+    if (ns_cap) {
+      P.split_count = S.d_split_count;
+      P.split_n = ns_cap;
+      P.split_rec = S.d_split_rec;
+      P.split_cap = S.split_cap;
+      P.split_thr = P.thr + 4e-3f < 1.f ? P.thr + 4e-3f : 2.f;
     }
   } else {
     // full frame: the block durations are measured on the first launch of the shape and every
@@ -1190,6 +1217,45 @@ std::vector<uint32_t> split_choose(const uint32_t *cost, uint32_t nb, uint32_t W
 // last plan) and attach them to P.  A split ray's records hold its back half: at most half the
 // longest chord of its wave in samples plus the drift of the t recurrence (t += tstep rounds by up
 // to ulp(t) / 2 per sample).
+// The records of `rays` split rays (their back halves' samples): at most half the longest chord of
+// a wave in samples plus the drift of the t recurrence (t += tstep rounds by up to ulp(t) / 2 per
+// sample) per ray; S.split_cap is set to that capacity.  Grown only (a launch in flight on this
+// stream may read the old buffers: waited for first).
+hipError_t split_records(vr_context::Schedule &S, const vr::RenderParams &P, uint32_t rays, hipStream_t stream) {
+  double pmax = 0.0, diag = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    pmax = std::max(pmax, (double)std::fabs(P.eye[i]) + std::fabs(P.bmin[i]));
+    diag += 4.0 * (double)P.bmin[i] * P.bmin[i];
+  }
+  diag = std::sqrt(diag);
+  const double est = diag / (double)P.tstep + 2.0;
+  const double drift = est * std::ldexp(1.0, std::ilogb(pmax + diag) - 24) / (double)P.tstep;
+  const uint32_t cap = (uint32_t)std::min(est * 0.5 + drift + 64.0, (double)P.max_steps);
+  const size_t rec_bytes = (size_t)rays * cap * 4 * sizeof(float);
+  if (rays > S.split_slots || rec_bytes > S.split_rec_bytes) {
+    VR_HIP(hipStreamSynchronize(stream));
+    for (void *q : {(void *)S.d_split_rec, (void *)S.d_split_hand, (void *)S.d_split_cnt, (void *)S.d_split_pix})
+      if (q) (void)hipFree(q);
+    S.d_split_rec = S.d_split_hand = nullptr;
+    S.d_split_cnt = nullptr;
+    S.d_split_pix = nullptr;
+    S.split_slots = 0;
+    S.split_rec_bytes = 0;
+    S.split_n = 0;
+    const uint32_t rays_alloc = rays + rays / 4;
+    const size_t bytes = rec_bytes + rec_bytes / 4;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&S.d_split_rec), bytes);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_hand), rays_alloc * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_cnt), rays_alloc * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_pix), rays_alloc * sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    S.split_slots = rays_alloc;
+    S.split_rec_bytes = bytes;
+  }
+  S.split_cap = cap;
+  return hipSuccess;
+}
+
 hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uint32_t nb,
                         const std::vector<uint32_t> *chosen, hipStream_t stream) {
   if (chosen) {  // a new plan
@@ -1201,39 +1267,8 @@ hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uin
       if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_split_list), nb * sizeof(uint32_t));
       if (e != hipSuccess) return e;
     }
-    double pmax = 0.0, diag = 0.0;
-    for (int i = 0; i < 3; ++i) {
-      pmax = std::max(pmax, (double)std::fabs(P.eye[i]) + std::fabs(P.bmin[i]));
-      diag += 4.0 * (double)P.bmin[i] * P.bmin[i];
-    }
-    diag = std::sqrt(diag);
-    const double est = diag / (double)P.tstep + 2.0;
-    const double drift = est * std::ldexp(1.0, std::ilogb(pmax + diag) - 24) / (double)P.tstep;
-    const uint32_t cap = (uint32_t)std::min(est * 0.5 + drift + 64.0, (double)P.max_steps);
     const uint32_t rays = n * 4u * (64u / (uint32_t)K);
-    const size_t rec_bytes = (size_t)rays * cap * 4 * sizeof(float);
-    if (rays > S.split_slots || rec_bytes > S.split_rec_bytes) {
-      // grown rarely (a plan with more split rays): a launch in flight on this stream may still read
-      // the old buffers -- wait for it before they go
-      VR_HIP(hipStreamSynchronize(stream));
-      for (void *q : {(void *)S.d_split_rec, (void *)S.d_split_hand, (void *)S.d_split_cnt, (void *)S.d_split_pix})
-        if (q) (void)hipFree(q);
-      S.d_split_rec = S.d_split_hand = nullptr;
-      S.d_split_cnt = nullptr;
-      S.d_split_pix = nullptr;
-      S.split_slots = 0;
-      S.split_rec_bytes = 0;
-      S.split_n = 0;
-      const uint32_t rays_alloc = rays + rays / 4;
-      const size_t bytes = rec_bytes + rec_bytes / 4;
-      hipError_t e = hipMalloc(reinterpret_cast<void **>(&S.d_split_rec), bytes);
-      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_hand), rays_alloc * sizeof(float));
-      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_cnt), rays_alloc * sizeof(int32_t));
-      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_pix), rays_alloc * sizeof(uint32_t));
-      if (e != hipSuccess) return e;
-      S.split_slots = rays_alloc;
-      S.split_rec_bytes = bytes;
-    }
+    VR_HIP(split_records(S, P, rays, stream));
     // the pinned plan buffers are rewritten only after their previous copy has run
     VR_HIP(hipStreamSynchronize(stream));
     for (uint32_t i = 0; i < nb; ++i) S.h_split_of[i] = -1;
@@ -1244,7 +1279,6 @@ hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uin
     VR_HIP(hipMemcpyAsync(S.d_split_of, S.h_split_of, nb * sizeof(int32_t), hipMemcpyHostToDevice, stream));
     if (n) VR_HIP(hipMemcpyAsync(S.d_split_list, S.h_split_list, n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
     S.split_n = n;
-    S.split_cap = cap;
     S.split_stale = false;
   }
   if (!S.split_n) return hipSuccess;
@@ -1398,6 +1432,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     const bool can_split = K > 1 && P.fast_shade && P.tame && F.mode >= 1 && F.ab_alias && !F.big && !P.wide_slot &&
                            P.views <= 1 && !P.steps;
     const char *force = can_split ? std::getenv("VR_SPLIT_FORCE") : nullptr;
+    // VR_SPLIT_SHORT=1: short launches (an image part of a multi-GPU frame) split their heaviest
+    // blocks inside the workgroup (SCHED 5)
+    F.split_short = can_split && env_flag("VR_SPLIT_SHORT");
     if (force) {
       static const blocks_fn fbf[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
                                        VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};

@@ -112,7 +112,10 @@ struct RenderParams {
   int32_t *split_cnt;             // per split ray: records B stored (-1: no ray)
   uint32_t *split_pix;            // per split ray: its output pixel index (B), or ~0
   float *split_hand;              // per split ray: A's opacity when it handed over, or -1
-  uint32_t split_n, split_cap;
+  uint32_t split_n, split_cap;     // split_n: the launch's extra workgroups (SCHED 4: the back halves;
+                                  // SCHED 5: the room for *split_count split blocks)
+  const uint32_t *split_count;    // SCHED 5 (in-workgroup split of a short launch): how many of the
+                                  // order's first blocks are split (written by the order kernel)
   float split_thr;                // B's own stop: its local opacity past thr + margin
   unsigned long long *steps;      // optional sample counter
   // sort-last slab launch (vr_render_slab): owned normalized z range [slab_z0,

@@ -507,20 +507,32 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t c) {
   return min(255u, e * 8u + m);
 }
 
+// split_n (optional): how many blocks lead the order with a duration of at least split_num / 16 of
+// the longest one (whole buckets, at most split_cap): the blocks a chord-split short launch marches
+// in two halves (vr_march.hip SCHED 5).
 __global__ __launch_bounds__(1024) void order_kernel(const uint32_t *__restrict__ cost, uint32_t n,
-                                                     uint32_t *__restrict__ order) {
+                                                     uint32_t *__restrict__ order, uint32_t *split_n,
+                                                     uint32_t split_num, uint32_t split_cap) {
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t cmax;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+  if (threadIdx.x == 0) cmax = 0;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    atomicAdd(&hist[cost_bucket(cost[i])], 1u);
+    if (split_n) atomicMax(&cmax, cost[i]);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {  // exclusive offsets, largest bucket first
-    uint32_t acc = 0;
+    uint32_t acc = 0, heavy = 0;
+    const uint32_t tb = split_n ? cost_bucket((uint32_t)(((uint64_t)cmax * split_num) >> 4)) : 256u;
     for (int b = 255; b >= 0; --b) {
       const uint32_t c = hist[b];
       hist[b] = acc;
       acc += c;
+      if ((uint32_t)b >= tb) heavy = acc;
     }
+    if (split_n) *split_n = heavy < split_cap ? heavy : split_cap;
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
@@ -598,12 +610,12 @@ __global__ __launch_bounds__(1024) void order_heavy_kernel(const uint32_t *__res
 // heavy_div 0: longest first (short launches); else the full-frame order of order_heavy_kernel
 // with tail = (tail_pct << 32) | resident workgroups.
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s, uint32_t heavy_div,
-                        uint64_t tail) {
+                        uint64_t tail, uint32_t *split_n, uint32_t split_num, uint32_t split_cap) {
   if (!n) return hipSuccess;
   if (heavy_div)
     hipLaunchKernelGGL(order_heavy_kernel, dim3(1), dim3(1024), 0, s, cost, n, heavy_div, (uint32_t)(tail >> 32),
                        (uint32_t)tail, order);
-  else hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
+  else hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order, split_n, split_num, split_cap);
   return hipGetLastError();
 }
 

@@ -703,19 +703,42 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n, int run) {
 // recording durations.
 // SCHED 4: a full frame in row-major order with the chord split of RenderParams::split_* (the
 // first split_n workgroups are the split blocks' back halves; split_composite_kernel follows).
+// SCHED 5: a short launch in longest-first order (as SCHED 1, timed) whose first *split_count blocks
+// are split inside their workgroups: each takes two workgroups, each of those two of its tiles, and a
+// tile's two waves march its front half (A, even wave) and back half (B, odd wave) at once; after a
+// workgroup barrier A composites B's records in order (DESIGN.md s9 "in-workgroup split").
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
-  constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
-  constexpr bool SPLIT = SCHED == 4;
+  constexpr bool TIMED = SCHED == 1 || SCHED == 2 || SCHED == 5;  // SCHED 3: the order only
+  constexpr bool SPLITW = SCHED == 5;
+  constexpr bool SPLIT = SCHED == 4 || SPLITW;
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
   SplitRole SR{0, 0, nullptr, 0};
   int slot = -1;
   uint32_t wgo;
-  if constexpr (SPLIT) {
+  int tile_in = wave;     // the tile of the block this wave marches
+  bool split_wg = false;  // SPLITW: this workgroup holds two split tiles of a block
+  int half = 0;
+  if constexpr (SPLITW) {
+    const uint32_t ns = *P.split_count;  // (uniform) written by the order kernel of this launch
+    uint32_t pos;
+    if (blockIdx.x < 2u * ns) {
+      pos = blockIdx.x >> 1;
+      half = (int)(blockIdx.x & 1u);
+      split_wg = true;
+      tile_in = (half << 1) | (wave >> 1);
+      SR.role = (wave & 1) ? 2 : 1;
+      slot = (int)((pos * 2u + (uint32_t)half) * 2u + (uint32_t)(wave >> 1));  // the tile's record slot
+    } else {
+      pos = blockIdx.x - ns;
+      if (pos >= P.sched_blocks) return;  // (whole workgroup) the grid's spare split capacity
+    }
+    wgo = P.wg_order[pos];
+  } else if constexpr (SPLIT) {
     if (blockIdx.x < P.split_n) {  // a back half (B)
       slot = (int)blockIdx.x;
       wgo = P.split_list[slot];
@@ -738,7 +761,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   const int view = (P.views > 1 && wgo >= P.view_blocks) ? 1 : 0;
   const uint32_t wg = view ? wgo - P.view_blocks : wgo;
   float *const out = view ? P.out2 : P.out;
-  const int tile = (int)wg * VR_WG_WAVES + wave;
+  const int tile = (int)wg * VR_WG_WAVES + tile_in;
   const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
   const int blk = tile >> 2, quad = tile & 3;
   const int ray = lane >> TS::LK;
@@ -767,7 +790,8 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   }
   // chord split: n_split = half the longest chord of the wave's rays in samples (wave-uniform; the
   // same in the block's two halves, which set up the same rays); this lane's ray's records
-  const size_t rslot = SPLIT ? ((size_t)(slot * VR_WG_WAVES + wave) * (64 / K) + (size_t)ray) : 0;
+  const size_t rslot = SPLITW ? ((size_t)slot * (64 / K) + (size_t)ray)
+                              : SPLIT ? ((size_t)(slot * VR_WG_WAVES + wave) * (64 / K) + (size_t)ray) : 0;
   if (SPLIT && SR.role) {
     const int est = R.alive ? (int)fminf((R.tfar - R.t) / P.tstep, 1.0e9f) : 0;
     SR.n_split = wave_max(est) >> 1;
@@ -791,7 +815,43 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
       march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
   }
 
-  if (SPLIT && SR.role == 2) {
+  if constexpr (SPLITW) {
+    if (split_wg) {  // (whole workgroup)
+      // B hands its record count to A through LDS; the barrier also orders B's record stores before
+      // A's loads (one workgroup, one CU)
+      __shared__ int split_cnt_lds[2][64];
+      if (SR.role == 2) {  // (wave-uniform: every lane of a group joins the DPP moves)
+        const int n = group_max_i<K>(SR.wrote, SR.wrote);
+        if ((lane & (K - 1)) == 0) split_cnt_lds[wave >> 1][ray] = n <= (int)P.split_cap ? n : -2;
+      }
+      __syncthreads();
+      if (SR.role == 1) {
+        // A: B's samples composited in order onto the front half (the reference's loop body, the
+        // early exit after each sample), K records per group iteration, 8 iterations' loads in flight
+        const int cnt = split_cnt_lds[wave >> 1][ray];
+        const int sub = lane & (K - 1);
+        if (cnt < 0) R.sr = R.sg = R.sb = __builtin_nanf("");  // (capacity exceeded: cannot happen, loud)
+        R.alive = active && cnt > 0 && !(R.sa > P.thr);
+        const float4 *rec = reinterpret_cast<const float4 *>(SR.rec);
+        for (int j = 0; __any(R.alive); j += 8 * K) {
+          float4 v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int q = j + i * K + sub;
+            v[i] = (R.alive && q < cnt) ? rec[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (R.alive) composite_group<K, 0>(P, R, (j + i * K + sub < cnt) ? 1.f : 0.f, v[i].x, v[i].y, v[i].z,
+                                               v[i].w, P.thr);
+          if (j + 8 * K >= cnt) R.alive = false;
+        }
+      }
+    }
+  }
+  if (SPLITW && SR.role == 2) {
+    // B: nothing to store (A wrote the pixel)
+  } else if (SPLIT && !SPLITW && SR.role == 2) {
     // B: how many records this ray's lanes stored (the group's largest), and its pixel
     const int n = group_max_i<K>(SR.wrote, SR.wrote);
     if ((lane & (K - 1)) == 0) {
@@ -806,12 +866,15 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     out[kk + 2 * plane] = R.sb;
     // A: the opacity to continue from when the ray did not stop (the reference goes on while
     // !(sum.a > thr)); -1: stopped, nothing to add
-    if (SPLIT && slot >= 0) P.split_hand[rslot] = (SR.role == 1 && !(R.sa > P.thr)) ? R.sa : -1.f;
+    if (SPLIT && !SPLITW && slot >= 0) P.split_hand[rslot] = (SR.role == 1 && !(R.sa > P.thr)) ? R.sa : -1.f;
   }
   if (TIMED) {  // this block's duration, for the next launch's schedule
     __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
+    if (threadIdx.x == 0 && half == 0) {
+      // (a split block: its first workgroup's duration doubled -- what the block would last unsplit,
+      // so that the next launch splits it again rather than taking it for a light block)
+      uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
+      if (split_wg) d *= 2u;
       P.wg_cost[wgo] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
       if (P.wg_start) P.wg_start[wgo] = (uint32_t)clk0;
     }
@@ -1100,7 +1163,7 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   // the chord-split kernel (SCHED 4) only where the host splits: lit, absorption = emission, the
   // default slot (vr_capi.hip split_plan)
   constexpr bool SPL = SCH && AB && MODE >= 1 && CAP == VR_LDS_CAP;
-  constexpr int S4 = SPL ? 4 : 0;
+  constexpr int S4 = SPL ? 4 : 0, S5 = SPL ? 5 : 0;
 #define VR_LAUNCH(KK, CNT, BG, SC, PAD)                                                                    \
   do {                                                                                                    \
     hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, PAD, s, P);        \
@@ -1114,6 +1177,9 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
     else VR_LAUNCH(K, VR_COUNT_K != 0, false, 0, 0);
   } else if (!VR_MARCH_FAST && sched) {  // the exact variant is built without the scheduled kernels
     return hipErrorInvalidValue;
+  } else if (P.split_n && P.split_count) {  // a short launch, its heaviest blocks split in-workgroup
+    if (!SPL || big || !sched || P.sched_full) return hipErrorInvalidValue;
+    VR_LAUNCH(K, false, false, S5, short_launch_lds_pad());
   } else if (P.split_n) {  // a full frame with its heaviest blocks split (not scheduled, 32-bit)
     if (!SPL || big || sched) return hipErrorInvalidValue;
     VR_LAUNCH(K, false, false, S4, 0);
@@ -1163,9 +1229,11 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
   if (P.views > 1 && (P.view_blocks != per_view || !P.out2)) return hipErrorInvalidValue;
-  if (P.split_n && (P.views > 1 || !P.split_list || !P.split_of || VR_MARCH_K == 1)) return hipErrorInvalidValue;
+  if (P.split_n && (P.views > 1 || VR_MARCH_K == 1 || !P.split_rec ||
+                    (P.split_count ? !P.wg_order : (!P.split_list || !P.split_of))))
+    return hipErrorInvalidValue;
   const dim3 grid(per_view * (P.views > 1 ? 2u : 1u) + P.split_n);  // (split: the back halves first)
-  if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || VR_MARCH_K == 1))
+  if (P.wg_order && (P.sched_blocks != grid.x - P.split_n || !P.wg_cost || VR_MARCH_K == 1))
     return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {
     case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);
