@@ -1486,7 +1486,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const hipError_t e = fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream);
       if (e != hipSuccess) throw HipError{e, "the march kernel launch (launch_march_k)"};
     }
-    if (P.split_n)  // the split rays' back halves composited onto their front halves, in order
+    // SCHED 4 (a full frame's split): the split rays' back halves composited onto their front halves,
+    // in order (a short launch's in-workgroup split, SCHED 5, composites inside the march kernel)
+    if (P.split_n && !P.split_count)
       VR_HIP(vr::launch_split_composite(P, P.split_n * 4u * (64u / (uint32_t)K), stream));
     time_mark(h, 1, stream);
     if (F.sched_copy) {  // a timed full frame: its block durations to the host, for the tail test

@@ -435,6 +435,7 @@ __global__ __launch_bounds__(256) void split_composite_kernel(const RenderParams
 
 hipError_t launch_split_composite(const RenderParams &P, uint32_t nrays, hipStream_t s) {
   if (!nrays) return hipSuccess;
+  if (!P.split_pix || !P.split_hand || !P.split_cnt || !P.split_rec || P.split_count) return hipErrorInvalidValue;
   hipLaunchKernelGGL(split_composite_kernel, dim3((nrays + 255) / 256), dim3(256), 0, s, P, nrays);
   return hipGetLastError();
 }
