@@ -458,8 +458,9 @@ def test_short_launch_split_is_bit_identical(monkeypatch, counter_clock, scene):
     """The in-workgroup chord split of a short launch (VR_SPLIT_SHORT=1, vr_march.hip SCHED 5): from
     the second launch of a part on, its heaviest blocks (by the previous launch's durations) are
     marched by two workgroups whose wave pairs take each tile's front and back halves, the back half's
-    samples composited in order by the front wave after a workgroup barrier.  Every launch of every
-    part assembles to the unsplit frame bit for bit, at every split threshold."""
+    samples composited in order by the front wave after a workgroup barrier, the back wave dropping
+    the rays the front one has stopped.  Every launch of every part assembles to the unsplit frame
+    bit for bit, at every split threshold and split index."""
     import torch
     from volume_renderer_amd import mex
     data = O.shell_volume(64)
@@ -477,8 +478,11 @@ def test_short_launch_split_is_bit_identical(monkeypatch, counter_clock, scene):
     ra, keep = mex.render_args(*args)
     W, H = 149, 101
     monkeypatch.setenv("VR_SPLIT_SHORT", "1")
-    for num in ("6", "1"):
+    # the split index: half of where the tile's rays stopped in the previous launch (default), or
+    # half the longest chord (VR_SPLIT_CHORD=1)
+    for num, chord in (("6", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("VR_SPLIT_SHORT_NUM", num)
+        monkeypatch.setenv("VR_SPLIT_CHORD", chord)
         for nparts, bc in ((2, 16), (4, 8)):
             maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
             for launch in range(3):

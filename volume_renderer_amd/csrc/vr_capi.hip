@@ -263,6 +263,7 @@ struct vr_context {
     uint32_t *d_split_pix = nullptr;
     size_t split_rec_bytes = 0;
     uint32_t *d_split_count = nullptr;  // short launches (SCHED 5): the order kernel's split count
+    uint32_t *d_split_len = nullptr;    // SCHED 5: per tile (4 per block), where its rays stopped
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -859,6 +860,12 @@ void free_schedules(vr_context *h) {
     if (kv.second.h_cost) (void)hipHostFree(kv.second.h_cost);
     if (kv.second.h_order) (void)hipHostFree(kv.second.h_order);
     if (kv.second.copied) (void)hipEventDestroy(kv.second.copied);
+    vr_context::Schedule &S = kv.second;
+    for (void *q : {(void *)S.d_split_list, (void *)S.d_split_of, (void *)S.d_split_rec, (void *)S.d_split_hand,
+                    (void *)S.d_split_cnt, (void *)S.d_split_pix, (void *)S.d_split_count, (void *)S.d_split_len})
+      if (q) (void)hipFree(q);
+    for (void *q : {(void *)S.h_split_list, (void *)S.h_split_of})
+      if (q) (void)hipHostFree(q);
   }
   h->sched.clear();
 }
@@ -996,6 +1003,10 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     if (const char *ev = std::getenv("VR_SPLIT_SHORT_NUM")) num = (uint32_t)std::min(16, std::max(1, std::atoi(ev)));
     if (F.split_short && nb >= 8) {
       hipError_t e = S.d_split_count ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&S.d_split_count), sizeof(uint32_t));
+      if (e == hipSuccess && !S.d_split_len) {
+        e = hipMalloc(reinterpret_cast<void **>(&S.d_split_len), (size_t)nb * 4u * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(S.d_split_len, 0, (size_t)nb * 4u * sizeof(uint32_t), stream);
+      }
       if (e == hipSuccess) e = split_records(S, P, (nb / 4) * 4u * (64u / (uint32_t)K), stream);
       if (e == hipSuccess) ns_cap = nb / 4;
       else vr_host::consume(e, "split buffers (the short launch runs unsplit)");
@@ -1014,6 +1025,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     }
     if (ns_cap) {
       P.split_count = S.d_split_count;
+      P.split_len = env_flag("VR_SPLIT_CHORD") ? nullptr : S.d_split_len;  // (A/B: half the chord)
       P.split_n = ns_cap;
       P.split_rec = S.d_split_rec;
       P.split_cap = S.split_cap;
@@ -1469,6 +1481,14 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       if (e == hipSuccess) P.wg_start = d_start;
       else vr_host::consume(e, "hipMalloc (VR_SCHED_DUMP start ticks; not recorded)");
     }
+    uint32_t *d_sdbg = nullptr;  // (SCHED 5) per split tile: A's / B's march ticks, the split index
+    const size_t sdbg_n = (size_t)P.sched_blocks * 4u * 3u;
+    if (dump && P.split_count) {
+      hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_sdbg), sdbg_n * 4);
+      if (e == hipSuccess) e = hipMemsetAsync(d_sdbg, 0, sdbg_n * 4, stream);
+      if (e == hipSuccess) P.split_dbg = d_sdbg;
+      else vr_host::consume(e, "VR_SCHED_DUMP split ticks (not recorded)");
+    }
     // VR_BLOCK_ROT_ROWS=r (A/B): the unscheduled launch starts at block row r of the row-major order
     // and wraps (the light top rows then fill the ramp-down of the heavy middle band)
     if (const char *ev = std::getenv("VR_BLOCK_ROT_ROWS")) {
@@ -1516,7 +1536,17 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
           std::fwrite(st.data(), 4, st.size(), f);
           std::fclose(f);
         }
+      if (P.split_dbg) {
+        std::vector<uint32_t> sd(sdbg_n);
+        VR_HIP(hipMemcpy(sd.data(), d_sdbg, sdbg_n * 4, hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen((std::string(dump) + ".split").c_str(), "ab")) {
+          std::fwrite(hdr, 4, 4, f);
+          std::fwrite(sd.data(), 4, sd.size(), f);
+          std::fclose(f);
+        }
+      }
     }
+    if (d_sdbg) (void)hipFree(d_sdbg);
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
     if (P.views > 1) {  // the general kernel renders one view per launch

@@ -93,6 +93,8 @@ struct RenderParams {
   const uint32_t *wg_order;
   uint32_t *wg_cost;
   uint32_t *wg_start;             // diagnostics (VR_SCHED_DUMP): each timed block's start tick (low 32 bits)
+  uint32_t *split_dbg;            // diagnostics (VR_SCHED_DUMP, SCHED 5): per split tile, A's and B's
+                                  // march ticks and the split index
   uint32_t sched_blocks;          // length of wg_order / wg_cost (must equal the launch's grid)
   uint32_t sched_full;            // 0: a short launch's schedule (longest first, timed); full frames
                                   // (occupancy-capped kernel, heavy blocks first or row-major): 1 timed,
@@ -116,7 +118,9 @@ struct RenderParams {
                                   // SCHED 5: the room for *split_count split blocks)
   const uint32_t *split_count;    // SCHED 5 (in-workgroup split of a short launch): how many of the
                                   // order's first blocks are split (written by the order kernel)
-  float split_thr;                // B's own stop: its local opacity past thr + margin
+  uint32_t *split_len;            // SCHED 5: per tile, the sample index its rays last needed (the
+                                  // previous launch's; 0 unknown) -- the split index is half of it
+  float split_thr;               // B's own stop: its local opacity past thr + margin
   unsigned long long *steps;      // optional sample counter
   // sort-last slab launch (vr_render_slab): owned normalized z range [slab_z0,
   // slab_z1), the margin of the chunk ownership test, the resident padded planes [slab_pk0,

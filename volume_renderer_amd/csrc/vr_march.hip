@@ -432,10 +432,15 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // records (SR.rec, compacted: the samples of empty-chunk leaps add exactly nothing and are not
 // stored) and composited locally only for B's own stop (opacity past P.split_thr); SR.wrote
 // returns the records this lane stored up to (B).
+// SCHED 5 (A and B waves of one workgroup): SR.stop points at the tile's per-ray flags in LDS --
+// A raises its ray's flag once the ray has stopped (opacity past thr), B reads it at each chunk
+// and drops the ray (its records would not be composited).
 struct SplitRole {
   int role, n_split;
   float *rec;  // this lane's ray's records (4 floats each)
   int wrote;
+  volatile int *stop;  // SCHED 5: the tile's flags (nullptr otherwise)
+  int ray;             // this lane's ray in the tile
 };
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false,
           bool SPLIT = false>
@@ -472,6 +477,17 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   // are the same whatever the chunk length (the staging never changes a result).
   int s0 = VR_CHUNK;
   while (__any(R.alive)) {
+    if constexpr (SPLIT) {
+      if (SR->stop) {  // SCHED 5: A publishes its stopped rays, B drops them (wave-uniform role)
+        if (SR->role == 1) {
+          if (sub == 0 && R.sa > thr) SR->stop[SR->ray] = 1;
+        } else if (role_b && SR->stop[SR->ray]) {
+          R.alive = false;
+          if constexpr (K > 1) R.mine = false;
+        }
+        if (!__any(R.alive)) break;
+      }
+    }
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
     int S;
     bool staged, partial;
@@ -717,7 +733,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   constexpr bool SPLITW = SCHED == 5;
   constexpr bool SPLIT = SCHED == 4 || SPLITW;
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
-  SplitRole SR{0, 0, nullptr, 0};
+  SplitRole SR{0, 0, nullptr, 0, nullptr, 0};
   int slot = -1;
   uint32_t wgo;
   int tile_in = wave;     // the tile of the block this wave marches
@@ -792,9 +808,27 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   // same in the block's two halves, which set up the same rays); this lane's ray's records
   const size_t rslot = SPLITW ? ((size_t)slot * (64 / K) + (size_t)ray)
                               : SPLIT ? ((size_t)(slot * VR_WG_WAVES + wave) * (64 / K) + (size_t)ray) : 0;
+  // SCHED 5: the tile's flags (A's stopped rays, for B) in LDS, cleared before either wave starts
+  if constexpr (SPLITW) {
+    __shared__ int split_stop_lds[2][64];
+    if (split_wg) {  // (whole workgroup)
+      if (threadIdx.x < 128) split_stop_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+      __syncthreads();
+      SR.stop = split_stop_lds[wave >> 1];
+      SR.ray = ray;
+    }
+  }
   if (SPLIT && SR.role) {
     const int est = R.alive ? (int)fminf((R.tfar - R.t) / P.tstep, 1.0e9f) : 0;
-    SR.n_split = wave_max(est) >> 1;
+    const int emax = wave_max(est);
+    SR.n_split = emax >> 1;
+    if (SPLITW && P.split_len) {
+      // SCHED 5: half the samples the tile's rays needed in the previous launch (where they stopped),
+      // so that A and B share the work actually done rather than the chord; B's part kept within
+      // the record capacity (split_records: half the longest chord + drift + 64)
+      const int used = (int)P.split_len[tile];  // (wave-uniform; A and B read the same entry)
+      if (used > 0) SR.n_split = max(used >> 1, emax - ((int)P.split_cap - 64));
+    }
     SR.rec = P.split_rec + rslot * (size_t)P.split_cap * 4u;
     if (SR.n_split < 1) {  // nothing to split in this wave: A marches it whole, B stores nothing
       if (SR.role == 2) R.alive = false;
@@ -816,21 +850,41 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   }
 
   if constexpr (SPLITW) {
+    if (split_wg && P.split_dbg && lane == 0) {  // diagnostics: this wave's march ticks
+      const size_t q = ((size_t)wg * VR_WG_WAVES + (size_t)tile_in) * 3u;
+      P.split_dbg[q + (SR.role == 2 ? 1 : 0)] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - clk0);
+      if (SR.role != 2) P.split_dbg[q + 2] = (uint32_t)SR.n_split;
+    }
+    // A's rays that stopped in its last chunk (B reads the flags at its chunk boundaries)
+    if (SR.stop && SR.role == 1 && (lane & (K - 1)) == 0 && R.sa > P.thr) SR.stop[ray] = 1;
     if (split_wg) {  // (whole workgroup)
       // B hands its record count to A through LDS; the barrier also orders B's record stores before
       // A's loads (one workgroup, one CU)
       __shared__ int split_cnt_lds[2][64];
+      __shared__ int split_end_lds[2][64];  // B: the sample index its ray stopped at
       if (SR.role == 2) {  // (wave-uniform: every lane of a group joins the DPP moves)
         const int n = group_max_i<K>(SR.wrote, SR.wrote);
-        if ((lane & (K - 1)) == 0) split_cnt_lds[wave >> 1][ray] = n <= (int)P.split_cap ? n : -2;
+        const int e = group_max_i<K>(R.nsteps, R.nsteps);
+        if ((lane & (K - 1)) == 0) {
+          split_cnt_lds[wave >> 1][ray] = n <= (int)P.split_cap ? n : -2;
+          split_end_lds[wave >> 1][ray] = e;
+        }
       }
       __syncthreads();
+      if (SR.role == 1 && P.split_len) {
+        // the samples this tile's rays needed: where A stopped them (before its cap), else where B did
+        const int a = group_max_i<K>(R.nsteps, R.nsteps);
+        const int used = !active ? 0 : a < SR.n_split ? a : split_end_lds[wave >> 1][ray];
+        const int m = wave_max(used);
+        if (lane == 0) P.split_len[tile] = (uint32_t)m;
+      }
       if (SR.role == 1) {
         // A: B's samples composited in order onto the front half (the reference's loop body, the
         // early exit after each sample), K records per group iteration, 8 iterations' loads in flight
         const int cnt = split_cnt_lds[wave >> 1][ray];
         const int sub = lane & (K - 1);
-        if (cnt < 0) R.sr = R.sg = R.sb = __builtin_nanf("");  // (capacity exceeded: cannot happen, loud)
+        if (cnt < 0 && active && !(R.sa > P.thr))  // (capacity exceeded where needed: cannot happen, loud)
+          R.sr = R.sg = R.sb = __builtin_nanf("");
         R.alive = active && cnt > 0 && !(R.sa > P.thr);
         const float4 *rec = reinterpret_cast<const float4 *>(SR.rec);
         for (int j = 0; __any(R.alive); j += 8 * K) {
@@ -847,6 +901,11 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
           if (j + 8 * K >= cnt) R.alive = false;
         }
       }
+    }
+    if (SR.role == 0 && P.split_len) {  // a tile marched whole: where its rays stopped
+      const int a = group_max_i<K>(R.nsteps, R.nsteps);
+      const int m = wave_max(active ? a : 0);
+      if (lane == 0) P.split_len[tile] = (uint32_t)m;
     }
   }
   if (SPLITW && SR.role == 2) {
