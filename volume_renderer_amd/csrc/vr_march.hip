@@ -36,6 +36,12 @@
 #ifndef VR_CHECK_WHOLE
 #define VR_CHECK_WHOLE 0
 #endif
+#ifndef VR_LIGHTS_HOIST
+#define VR_LIGHTS_HOIST 1  // tame launches: the first light pair held in registers across the march
+#endif
+#ifndef VR_REFL_HOIST
+#define VR_REFL_HOIST 1  // tame launches: the reflection's single voxel read once per wave (sample_at)
+#endif
 #ifndef VR_ADAPTIVE_S
 #define VR_ADAPTIVE_S 1
 #endif
@@ -159,7 +165,7 @@ struct ChunkStats {
 template <int MODE, bool AB_ALIAS, bool SHARE2, bool BIG, bool NANCHK>
 __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L, const Box &B, bool staged, bool whole,
                                           const f3 pos, const f3 o, float &r, float &gg, float &b, float &alpha,
-                                          bool &shaded) {
+                                          bool &shaded, float rv = 0.f, const DevLight *pre = nullptr) {
   const DevTex &E = P.em;
   const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
   const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
@@ -310,13 +316,14 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     }
     float refl;
     if constexpr (TAME) {  // the emission sample or the single voxel, selected by a 32-bit mask (v_bfi)
-      const float v = voxel0(P.re.p);
+      // VR_REFL_HOIST: the single voxel loaded once per wave before the march (rv), not per sample
+      const float v = VR_REFL_HOIST ? rv : voxel0(P.re.p);
       const uint32_t m = P.re_mask;
       refl = P.fr * __uint_as_float((__float_as_uint(em_s) & m) | (__float_as_uint(fmaf(0.5f, v - v, v)) & ~m));
     } else {
       refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
     }
-    shade_lights<VR_MARCH_FAST, TAME>(P, g, pos, o, refl, ir, ig, ib);
+    shade_lights<VR_MARCH_FAST, TAME>(P, g, pos, o, refl, ir, ig, ib, pre);
   }
   r = fmaf(eds, P.color[0], ir) * alpha;
   gg = fmaf(eds, P.color[1], ig) * alpha;
@@ -476,6 +483,28 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   // instead of always VR_CHUNK halved until it fits: fewer box reductions per chunk.  The samples
   // are the same whatever the chunk length (the staging never changes a result).
   int s0 = VR_CHUNK;
+  // the tame reflection's single voxel (sample_at), held in a register across the march: an opaque
+  // copy, so that the compiler does not re-issue the invariant load in every sample
+  float rv = 0.f;
+  if constexpr (!NANCHK && VR_REFL_HOIST) {
+    if (P.tame && P.re.p) rv = voxel0(P.re.p);
+    asm volatile("" : "+v"(rv));
+  }
+  // VR_LIGHTS_HOIST: the first light pair likewise (shade_fast), when the frame has two or more
+  DevLight pre2[2];
+  const DevLight *pre = nullptr;
+  // (only where the registers fit without lowering occupancy or spilling: not K = 1, the slab, split
+  // or counter variants, nor the 64-bit, separate-absorption or full-gradient-tap ones)
+  if constexpr (!NANCHK && VR_LIGHTS_HOIST && MODE != 0 && K > 1 && AB_ALIAS && SHARE2 && !BIG && !SLAB &&
+                !SPLIT && !COUNT) {
+    const bool two = P.num_lights >= 2;
+    for (int j = 0; j < 2; ++j) {
+      pre2[j] = two ? light_at(P, j) : DevLight{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+v"(pre2[j].px), "+v"(pre2[j].py), "+v"(pre2[j].pz), "+v"(pre2[j].cr), "+v"(pre2[j].cg),
+                   "+v"(pre2[j].cb));
+    }
+    if (two) pre = pre2;
+  }
   while (__any(R.alive)) {
     if constexpr (SPLIT) {
       if (SR->stop) {  // SCHED 5: A publishes its stopped rays, B drops them (wave-uniform role)
@@ -581,7 +610,8 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         }
         float r, gg, b, alpha;
         bool shaded;
-        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded);
+        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded,
+                                                       rv, pre);
         if (COUNT) {
           ++C.iter;
           C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
@@ -612,7 +642,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         bool shaded = false;
         if (take) {
           sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, WC || (!VR_WHOLE_SPLIT && whole), R.pos,
-                                                         R.o, r, gg, b, alpha, shaded);
+                                                         R.o, r, gg, b, alpha, shaded, rv, pre);
         }
         if (COUNT) {
           ++C.iter;

@@ -651,7 +651,8 @@ __device__ __forceinline__ float voxel0(const float *p) {
 // cosine's rounding there) -- where the hybrid shading (VR_FAST_HYBRID) takes XN + XG.
 template <bool TAME, bool XN, bool XG, bool NEED>
 __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
-                                          const float refl, float &ir, float &ig, float &ib, bool &need) {
+                                          const float refl, float &ir, float &ig, float &ib, bool &need,
+                                          const DevLight *pre = nullptr) {
   // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
   float ginv;
   if constexpr (XN) ginv = rcp_sqrt_cr(dot3(g, g));  // the oracle's 1 / sqrtf(g.g), bit for bit
@@ -702,7 +703,9 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
     // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
     for (; i + 1 < P.num_lights; i += 2) {
-      const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
+      // pre: the first pair held in registers by the caller (vr_march.hip VR_LIGHTS_HOIST)
+      const DevLight L0 = (pre && i == 0) ? pre[0] : light_at(P, i);
+      const DevLight L1 = (pre && i == 0) ? pre[1] : light_at(P, i + 1);
       const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
       const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
       const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
@@ -776,7 +779,8 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
 
 template <bool FAST, bool TAME = false>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
-                                             const float refl, float &ir, float &ig, float &ib) {
+                                             const float refl, float &ir, float &ig, float &ib,
+                                             const DevLight *pre = nullptr) {
 #if !VR_FAST_COS
   if constexpr (FAST) {
     // VR_FAST_COS 0 (parity ablation): the normal and the angle cosines in the exact variant's
@@ -835,7 +839,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     }
 #else
     bool unused = false;
-    shade_fast<TAME, VR_FAST_NX, VR_FAST_GX, false>(P, g, pos, o, refl, ir, ig, ib, unused);
+    shade_fast<TAME, VR_FAST_NX, VR_FAST_GX, false>(P, g, pos, o, refl, ir, ig, ib, unused, pre);
 #endif
   } else {
     // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.
