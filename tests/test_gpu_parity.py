@@ -78,6 +78,27 @@ def test_hg_two_lights_compute_gradient(monkeypatch, counter_clock):
     r.delete()
 
 
+@pytest.mark.parametrize("nlights", [1, 3, 4])
+@pytest.mark.parametrize("refl", ["voxel", "emission"])
+def test_light_counts_and_reflection(monkeypatch, counter_clock, nlights, refl):
+    """Odd and even light counts (the march holds the first light pair and the single reflection
+    voxel in registers, vr_march.hip VR_LIGHTS_HOIST / VR_REFL_HOIST; the rest come from the light
+    list) with the default single-voxel reflection (a value other than 1) or the emission volume as
+    the reflection texture: parity with the oracle on every render (harness)."""
+    from harness import install
+    tee = install(monkeypatch)
+    v = vr.Volume(O.shell_volume(40))
+    r = ex1_renderer(v, res=(72, 64))
+    pos = [[500, 1000, 550], [0, 550, 90], [-300, 200, 700], [90, -400, 20]]
+    col = [[0, 1, 1], [1, 0.5, 1], [0.3, 0.9, 0.2], [0.6, 0.6, 0.1]]
+    r.LightSources = [vr.LightSource(pos[i], col[i]) for i in range(nlights)]
+    r.VolumeReflection = v if refl == "emission" else vr.Volume(np.full((1, 1, 1), 0.7, np.float32))
+    img = r.render()
+    assert np.isfinite(img).all() and img.max() > 0
+    print("lights", nlights, refl, tee.renders[-1][2])
+    r.delete()
+
+
 def test_lookup_gradient_then_compute(monkeypatch, counter_clock):
     """examples/example1_grad.m: precomputed gradient volumes, then resetGradientVolumes."""
     from harness import install
