@@ -8,7 +8,7 @@ import collections
 import re
 import sys
 
-path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/probe.s"
+path = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/tmp/probe.s"
 s = open(path).read()
 name = re.search(r"(_ZN2vr4fast12march_kernelILi2ELi1ELb1ELb0ELb1ELb0ELi1664ELi0EEEvNS_12RenderParamsE):", s).group(1)
 body = s[s.index(name + ":"):s.index(".Lfunc_end", s.index(name + ":"))].split("\n")
@@ -39,6 +39,10 @@ for h in hdrs:
         best = (h, nan, lp)
 hdr, _, loop = best
 hot = [b for b in loop if not any(x.startswith(("v_lshl_add_u64", "v_mad_u64_u32")) for x in b["ins"])]
+# the lights past the first pair (held in registers since round 4) are loaded by index inside the loop:
+# their blocks are off the common path of a two-light frame (--all keeps them)
+if "--all" not in sys.argv:
+    hot = [b for b in hot if not any(x.startswith("s_load_") for x in b["ins"])]
 c = collections.Counter(x.split()[0] for b in hot for x in b["ins"])
 valu = sum(n for k, n in c.items() if k.startswith("v_"))
 slow = sum(n for k, n in c.items() if k.startswith(("v_cmp", "v_cvt", "v_floor", "v_rndne", "v_fract", "v_med3",
@@ -48,7 +52,7 @@ trans = sum(n for k, n in c.items() if k.startswith(("v_rsq", "v_sqrt", "v_exp",
 print(f"loop BB{hdr}: {len(loop)} blocks, common path {len(hot)}: instructions {sum(c.values())}, VALU {valu} "
       f"(slow class {slow}, transcendental {trans}), readlane {c['v_readlane_b32']}, s_nop {c['s_nop']}, "
       f"scratch {c['scratch_load_dword'] + c['scratch_load_dwordx2']}, LDS {sum(n for k, n in c.items() if k.startswith('ds_'))}")
-if len(sys.argv) > 2 and sys.argv[2] == "--dump":
+if "--dump" in sys.argv:
     for b in hot:
         print(b["name"], b["hdr"][:80])
         for x in b["ins"]:
