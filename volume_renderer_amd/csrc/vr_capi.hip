@@ -1392,7 +1392,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const uint64_t n = bx->bytes / sizeof(float);
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
-      gv->bytes = n * (VR_GVEC_ZPAIR ? 8 : 4) * sizeof(float);
+      gv->bytes = n * (VR_GVEC_ZPAIR == 2 ? 3 : VR_GVEC_ZPAIR ? 8 : 4) * sizeof(float);
       const hipError_t ea = vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device);
       if (ea == hipSuccess) {
         for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);

@@ -8,7 +8,8 @@ namespace vr {
 // Layout of the interleaved lookup gradient (RenderParams::gvec).  0 (default): (gx, gy, gz, 0) per
 // padded voxel.  1 (A/B, round 4): z-paired -- entry i is 32 bytes, voxel i and voxel i + pxy (the
 // next plane), so a lookup's eight corners lie in two 64-byte runs instead of four 32-byte runs;
-// measured slower (C3 37.7 vs 36.4 ms: twice the footprint), DESIGN.md s8.
+// measured slower (C3 37.7 vs 36.4 ms: twice the footprint), DESIGN.md s8.  2 (A/B): packed (gx, gy,
+// gz), 12 bytes per voxel -- measured slower as well (C3 37.7 vs 34.3 ms: smaller, unaligned loads).
 #ifndef VR_GVEC_ZPAIR
 #define VR_GVEC_ZPAIR 0
 #endif

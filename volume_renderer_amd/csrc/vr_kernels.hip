@@ -460,13 +460,26 @@ __global__ __launch_bounds__(256) void interleave3z_kernel(const float *__restri
   }
 }
 
+// The packed interleave (VR_GVEC_ZPAIR 2): (a, b, c) of voxel i at floats 3i .. 3i + 2
+__global__ __launch_bounds__(256) void interleave3p_kernel(const float *__restrict__ a, const float *__restrict__ b,
+                                                           const float *__restrict__ c, float *__restrict__ out,
+                                                           uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    out[3 * i] = a[i];
+    out[3 * i + 1] = b[i];
+    out[3 * i + 2] = c[i];
+  }
+}
+
 // out: n entries of the VR_GVEC_ZPAIR layout (pxy: the plane pitch of the padded volume)
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, uint64_t pxy,
                               hipStream_t s) {
   if (!n) return hipSuccess;
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 262144) blocks = 262144;
-  if (VR_GVEC_ZPAIR)
+  if (VR_GVEC_ZPAIR == 2)
+    hipLaunchKernelGGL(interleave3p_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c, out, n);
+  else if (VR_GVEC_ZPAIR)
     hipLaunchKernelGGL(interleave3z_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
                        reinterpret_cast<float4 *>(out), n, pxy);
   else
