@@ -110,9 +110,14 @@ def main():
     n, W, H = args.volume, args.width, args.height
 
     # ---- inputs, resident in HBM before timing ------------------------------------------------
+    # the volume is made on rank 0 only (what one H2D upload of the MATLAB array gives) and, at N > 1,
+    # broadcast once to every rank's replica over RCCL, timed apart from the frames
     vol_t = torch.empty(n * n * n, dtype=torch.float32, device=dev)
-    mex.synth_shell_device(vol_t.data_ptr(), n, sptr)
+    if rank == 0:
+        mex.synth_shell_device(vol_t.data_ptr(), n, sptr)
     torch.cuda.synchronize(dev)
+    from volume_renderer_amd import parallel
+    bcast = parallel.broadcast_volume(vol_t, world, rank) if world > 1 else None
     em = mex.DeviceVolume(vol_t.data_ptr(), (n, n, n), last_update=10, owner=vol_t)
     refl = vr.Volume(1)          # VolumeRender.m:131 default VolumeReflection
     refl.TimeLastUpdate = np.uint64(5)
@@ -165,7 +170,11 @@ def main():
             torch.cuda.synchronize(dev)
         finally:
             del os.environ["VR_COUNT_PROD"]
-        prod_stats = {"kernel": mex.last_march_kernel(),
+        kn = mex.last_march_kernel() or ""
+        if "march_kernel<1," in kn:  # a normal build counts at K = 1 only (VR_COUNT_PROD needs VR_COUNT_K=1)
+            print("bench.py: --chunk-stats-k needs a VR_COUNT_K=1 build; the counted launch ran at K = 1",
+                  file=sys.stderr)
+        prod_stats = {"kernel": kn,
                       "chunks_staged_leaped_global": [int(v) for v in steps_t[2:5].tolist()],
                       "wave_iterations_total_lit": [int(v) for v in steps_t[5:7].tolist()],
                       "staged_chunks_by_S_32_16_8_4": [int(v) for v in steps_t[40:44].tolist()],
@@ -211,7 +220,6 @@ def main():
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
     ranks = None
     if world > 1:  # per-rank kernel and gather + assembly times, all-gathered to rank 0
-        from volume_renderer_amd import parallel
         gath_ms = [b.elapsed_time(g) for (_, b), g in zip(ev, evg)]
         ranks = parallel.rank_report(t_kernel_s * 1e3, sum(gath_ms) / len(gath_ms), world, rank, device=dev)
 
@@ -339,6 +347,9 @@ def main():
                                            "(independent movie frames overlap their tails); not `value`"}
         if ranks is not None:
             result["ranks"] = ranks
+        if bcast is not None:
+            result["upload_broadcast_ms"] = bcast["ms"]
+            result["volume_broadcast"] = bcast
         if prod_stats is not None:
             result["chunk_stats_production_k"] = prod_stats
         if sim is not None:

@@ -9,7 +9,8 @@
  * references + MATLAB mex, /root/reference/src/C/vr/volumeRender_kernel.cu) cannot be built or run
  * in this image and ships no tests, golden images or fixtures.  This file
  * is a line-by-line restatement of the reference's arithmetic; the only reference-pinned values
- * on this path are the Henyey-Greenstein LUT known answers (see oracle/vr_oracle_hg.c).
+ * on this path are the Henyey-Greenstein LUT known answers (the LUT restatement is
+ * oracle/vr_oracle_host.c; tests/test_oracle.py checks it against them).
  *
  * Arithmetic contract (shared with the HIP kernel, written out in DESIGN.md section 4):
  *   - IEEE fp32 (or fp64 for the envelope build, -DOR_DOUBLE), compiled with -ffp-contract=off.

@@ -88,6 +88,51 @@ def _report_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _bcast_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0 holds the volume (V_shell), the others an empty replica buffer of the same size
+        vol = torch.from_numpy(np.ascontiguousarray(O.shell_volume(40).reshape(-1, order="F")))
+        if rank != 0:
+            vol = torch.full_like(vol, -1.0)
+        rep = parallel.broadcast_volume(vol, world, rank)
+        q.put((rank, vol.numpy().copy(), rep))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_volume_broadcast_replicates_rank0_bytes():
+    """bench.py at N > 1 (SURVEY.md 8e "Collectives"): the volume is made on rank 0 only and broadcast
+    once (parallel.broadcast_volume, RCCL on the GPU, gloo here at world 2); every rank then holds rank
+    0's bytes exactly, and the report carries the bytes, the time and the replicas' checksum check."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (v, rep)) for r, v, rep in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = np.ascontiguousarray(O.shell_volume(40).reshape(-1, order="F"))
+    for r in range(world):
+        v, rep = got[r]
+        assert np.array_equal(v.view(np.uint32), ref.view(np.uint32)), r
+        assert rep["bytes"] == ref.nbytes and rep["ranks"] == world and rep["replicas_identical"] is True
+        assert rep["ms"] >= 0 and rep["backend"] == "gloo"
+    # a replica that differs is caught by the checksum (order-sensitive)
+    a = torch.from_numpy(ref.copy())
+    b = a.clone()
+    i, j = int(np.argmax(ref)), int(np.argmin(ref))
+    assert ref[i] != ref[j]
+    b[[i, j]] = b[[j, i]]
+    assert torch.equal(parallel.volume_checksum(a), parallel.volume_checksum(a.clone()))
+    assert not torch.equal(parallel.volume_checksum(a), parallel.volume_checksum(b))
+
+
 def test_rank_report_attributes_a_multi_gpu_frame():
     """bench.py's per-rank report at N > 1 (parallel.rank_report), over gloo at world 2: every rank's
     kernel and gather + assembly times reach rank 0 in rank order, with their max / min and the

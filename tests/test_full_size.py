@@ -278,18 +278,18 @@ def test_c4_two_channels_stereo_1920x1080():
     """example3.m: a main channel (V_shell(1024), colour [1 1 1], Fe = Fa = Fr = 1) and a structure
     channel (a second field, colour [0 1 0], Fe 0.5) with one light, LUT 64, thr 0.95, f 4.5,
     rotate(90,0,0) then rotate(-15,15,15), off-axis stereo CameraXOffset 0.06 (both eyes at
-    1920 + delta columns before the crop) -- all four views marched by vr_render_channels.  Each
+    1920 + delta = 1936 columns before the crop, delta from ImageResolution(2) = 1080) -- all four views marched by vr_render_channels.  Each
     channel x eye is checked against its own oracle session (the reference renders the channels
     one after the other, each right after its sync).  The 4-GPU split of the config: a channel's
     view rendered as a 4-part partition assembles to the fused launch's image bit for bit."""
     n, W, H = 1024, 1920, 1080
     R = O.rotation(-15, 15, 15, R=O.rotation(90, 0, 0))
     f, dist, xoff = 4.5, 6.0, 0.06
-    base = xoff / 2
-    fov = 2 * np.arctan(1 / f)
-    delta = base * W / (2 * f * np.tan(fov / 2))
-    delta = int(np.floor(abs(delta) + 0.5))
-    res = [H, W + delta]
+    # the product's VolumeRender.m:278-283 mirror: delta from ImageResolution(2) = H -> 16 columns
+    from volume_renderer_amd.volume_render import stereo_geometry
+    base, delta, res = stereo_geometry(xoff, f, [W, H])
+    assert delta == 16 and list(res) == [H, W + 16]
+    res = [int(v) for v in res]
     lut = stamped(vr.Volume(vr.HenyeyGreenstein(64)), 7)
     refl = stamped(vr.Volume(1), 5)
     chans, oracles, keep = [], [], []

@@ -379,7 +379,7 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
         r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
     imgs = {}
     keys = ("VR_NO_LDS", "VR_NO_EMPTY_SKIP", "VR_TILE_MODE", "VR_FORCE_BIG", "VR_NO_SMALL_LUT", "VR_WIDE_SLOT",
-            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS", "VR_SPLIT_FORCE")
+            "VR_NO_GVEC", "VR_DEPTH_LANES", "VR_SCHED", "VR_XCD_RUN", "VR_BLOCK_ROT_ROWS")
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
@@ -392,10 +392,7 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
                       ("k1_sched", {"VR_DEPTH_LANES": "1", "VR_SCHED": "1"}),
                       ("xcd_run2", {"VR_XCD_RUN": "2"}), ("k4_xcd_run4", {"VR_DEPTH_LANES": "4", "VR_XCD_RUN": "4"}),
                       ("rot3", {"VR_BLOCK_ROT_ROWS": "3"}), ("k4_rot2", {"VR_DEPTH_LANES": "4", "VR_BLOCK_ROT_ROWS": "2"}),
-                      ("k1_nogvec", {"VR_DEPTH_LANES": "1", "VR_NO_GVEC": "1"}),
-                      ("split_all", {"VR_SPLIT_FORCE": "1"}), ("split_third", {"VR_SPLIT_FORCE": "0.33"}),
-                      ("k2_split", {"VR_DEPTH_LANES": "2", "VR_SPLIT_FORCE": "1"}),
-                      ("k4_split", {"VR_DEPTH_LANES": "4", "VR_SPLIT_FORCE": "0.5"})]:
+                      ("k1_nogvec", {"VR_DEPTH_LANES": "1", "VR_NO_GVEC": "1"})]:
         for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, val in env.items():
@@ -407,117 +404,6 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
     assert base.max() > 0
     for name, img in imgs.items():
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
-    r.delete()
-
-
-@pytest.mark.parametrize("k", ["2", "4"])
-@pytest.mark.parametrize("scene", ["hg2", "lookup", "dense"])
-def test_chord_split_is_bit_identical(monkeypatch, counter_clock, scene, k):
-    """The chord split (vr_march.hip SCHED 4): the blocks' back halves marched by their
-    own workgroups from the replayed recurrence, their samples stored and composited onto the front
-    halves in order by split_composite_kernel -- the image of one pass, bit for bit, for every
-    fraction of split blocks, both gradient modes and the depth lanes of the full frame and of a
-    part.  `dense`: an opacity-heavy volume whose rays mostly stop early (in the front half, or in
-    the back half past B's own stop)."""
-    from volume_renderer_amd import mex
-    from harness import install
-    monkeypatch.setenv("VR_DEPTH_LANES", k)
-    tee = install(monkeypatch)
-    data = O.shell_volume(64)
-    if scene == "dense":
-        data = np.asfortranarray(data * 2 + 0.02, dtype=np.float32)
-    v = vr.Volume(data)
-    r = ex1_renderer(v, res=(133, 101))
-    if scene == "lookup":
-        r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
-    monkeypatch.setenv("VR_SPLIT", "0")
-    base = r.render()
-    assert not mex.last_march_kernel().endswith(", 4>")
-    monkeypatch.delenv("VR_SPLIT")
-    for f in ("1", "0.5", "0.1"):
-        monkeypatch.setenv("VR_SPLIT_FORCE", f)
-        img = r.render()
-        assert mex.last_march_kernel().endswith(", 4>"), (f, mex.last_march_kernel())
-        assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), (scene, k, f)
-    monkeypatch.delenv("VR_SPLIT_FORCE")
-    assert base.max() > 0 and len(tee.renders) == 4  # every render also checked against the oracle
-    r.delete()
-
-
-def test_chord_split_in_partitions(monkeypatch, counter_clock):
-    """The chord split inside the image partition's part launches (each part its own launch of the
-    split kernel, as a rank would run it): the parts assemble to the unsplit full frame bit for bit."""
-    import torch
-    from volume_renderer_amd import mex
-    v = vr.Volume(O.shell_volume(48))
-    r = ex1_renderer(v, res=(131, 93))
-    monkeypatch.setenv("VR_DEPTH_LANES", "4")
-    full = r.render()
-    args = (r.LightSources, r.VolumeIllumination,
-            np.float32([r.FactorEmission, r.FactorReflection, r.FactorAbsorption]), np.float32(r.ElementSizeUm),
-            np.uint64([93, 131]), np.flip(r.RotationMatrix, 0).astype(np.float32),
-            np.float32([0, r.FocalLength, r.DistanceToObject]), np.float32(r.OpacityThreshold), np.float32(r.Color))
-    ra, keep = mex.render_args(*args)
-    W, H = 131, 93
-    monkeypatch.setenv("VR_SPLIT_FORCE", "0.5")
-    for nparts, bc in ((2, 16), (4, 8)):
-        maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
-        parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
-        for p in range(nparts):
-            mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts))
-            assert mex.last_march_kernel().endswith(", 4>"), mex.last_march_kernel()
-        out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
-        mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
-        torch.cuda.synchronize()
-        img = out.cpu().numpy().reshape(-1)
-        assert np.array_equal(img.view(np.uint32), full.reshape(-1, order="F").view(np.uint32)), (nparts, bc)
-    r.delete()
-
-
-@pytest.mark.parametrize("scene", ["hg2", "lookup", "dense"])
-def test_short_launch_split_is_bit_identical(monkeypatch, counter_clock, scene):
-    """The in-workgroup chord split of a short launch (VR_SPLIT_SHORT=1, vr_march.hip SCHED 5): from
-    the second launch of a part on, its heaviest blocks (by the previous launch's durations) are
-    marched by two workgroups whose wave pairs take each tile's front and back halves, the back half's
-    samples composited in order by the front wave after a workgroup barrier, the back wave dropping
-    the rays the front one has stopped.  Every launch of every part assembles to the unsplit frame
-    bit for bit, at every split threshold and split index."""
-    import torch
-    from volume_renderer_amd import mex
-    data = O.shell_volume(64)
-    if scene == "dense":
-        data = np.asfortranarray(data * 2 + 0.02, dtype=np.float32)
-    v = vr.Volume(data)
-    r = ex1_renderer(v, res=(149, 101))
-    if scene == "lookup":
-        r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = v.grad()
-    full = r.render()
-    args = (r.LightSources, r.VolumeIllumination,
-            np.float32([r.FactorEmission, r.FactorReflection, r.FactorAbsorption]), np.float32(r.ElementSizeUm),
-            np.uint64([101, 149]), np.flip(r.RotationMatrix, 0).astype(np.float32),
-            np.float32([0, r.FocalLength, r.DistanceToObject]), np.float32(r.OpacityThreshold), np.float32(r.Color))
-    ra, keep = mex.render_args(*args)
-    W, H = 149, 101
-    monkeypatch.setenv("VR_SPLIT_SHORT", "1")
-    # the split index: half of where the tile's rays stopped in the previous launch (default), or
-    # half the longest chord (VR_SPLIT_CHORD=1)
-    for num, chord in (("6", "0"), ("1", "0"), ("1", "1")):
-        monkeypatch.setenv("VR_SPLIT_SHORT_NUM", num)
-        monkeypatch.setenv("VR_SPLIT_CHORD", chord)
-        for nparts, bc in ((2, 16), (4, 8)):
-            maxc = max(mex.partition_columns(W, mex.partition(bc, p, nparts)) for p in range(nparts))
-            for launch in range(3):
-                parts = torch.zeros((nparts, 3, maxc, H), dtype=torch.float32, device="cuda")
-                for p in range(nparts):
-                    mex.render_device(r.objectHandle, ra, parts[p].data_ptr(), mex.partition(bc, p, nparts))
-                    name = mex.last_march_kernel()
-                    assert name.endswith(", 5>"), name
-                out = torch.zeros((3, W, H), dtype=torch.float32, device="cuda")
-                mex.assemble_partitions(parts.data_ptr(), W, H, bc, nparts, maxc, out.data_ptr())
-                torch.cuda.synchronize()
-                img = out.cpu().numpy().reshape(-1)
-                assert np.array_equal(img.view(np.uint32), full.reshape(-1, order="F").view(np.uint32)), \
-                    (scene, num, nparts, launch)
     r.delete()
 
 

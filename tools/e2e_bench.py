@@ -103,9 +103,8 @@ def main():
            "p_render_ms": round(med(p_render), 2)}
     # stereo pair (example3.m CameraXOffset 0.06, f = 3 here): the reference's two renders vs the
     # fused launch (vr_render_stereo); each at the widened resolution [H, W + delta]
-    base = 0.03
-    fov = 2 * np.arctan(1 / 3.0)
-    delta = int(np.floor(base * W / (2 * 3.0 * np.tan(fov / 2)) + 0.5))
+    from volume_renderer_amd.volume_render import stereo_geometry
+    base, delta, _ = stereo_geometry(0.06, 3.0, [W, H])  # delta from ImageResolution(2) = H
     scall = list(call)
     scall[6] = np.uint64([H, W + delta])
 

@@ -28,8 +28,8 @@ def scene_def(name):
     if name.startswith("c4"):
         W0, H = 1920, 1080
         f, dist, xoff = 4.5, 6.0, 0.06
-        base = xoff / 2
-        delta = int(np.floor(abs(base * W0 / (2 * f * np.tan(np.arctan(1 / f)))) + 0.5))
+        from volume_renderer_amd.volume_render import stereo_geometry
+        base, delta, _ = stereo_geometry(xoff, f, [W0, H])  # delta from ImageResolution(2) = H: 16
         struct = name == "c4_struct"
         return dict(gen="structure" if struct else "shell", n=1024, W=W0 + delta, H=H,
                     R=O.rotation(-15, 15, 15, R=O.rotation(90, 0, 0)), props=[-base, f, dist], thr=0.95,

@@ -70,15 +70,14 @@ VR_DECL_MARCH(fast)
 VR_DECL_MARCH(exact)
 #undef VR_DECL_MARCH
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s, uint32_t heavy_div,
-                        uint64_t tail, uint32_t *split_n = nullptr, uint32_t split_num = 0, uint32_t split_cap = 0);
+                        uint64_t tail);
 hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
-hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, uint64_t pxy,
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n,
                               hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
-hipError_t launch_split_composite(const RenderParams &P, uint32_t nrays, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
 hipError_t launch_synth_shell(float *out, uint64_t n, uint64_t z_first, uint64_t nz, hipStream_t s);
@@ -250,20 +249,6 @@ struct vr_context {
     uint32_t *h_order = nullptr;  // pinned: a host-computed order (VR_SCHED_SHIFT / VR_SCHED_ROWS)
     hipEvent_t copied = nullptr;
     bool copy_pending = false, decided = false, tail = false;
-    // chord split of the heaviest blocks (split_choose / split_attach; frames without a tail
-    // schedule): the blocks' back halves (d_split_list), the block -> slot map (d_split_of, -1: not
-    // split), per split ray the back half's records and the hand-over state; pinned plan staging
-    bool split_stale = false;  // a plan chosen from new durations, not yet attached
-    std::vector<uint32_t> split_plan;
-    uint32_t split_n = 0, split_slots = 0, split_cap = 0;
-    uint32_t *d_split_list = nullptr, *h_split_list = nullptr;
-    int32_t *d_split_of = nullptr, *h_split_of = nullptr;
-    float *d_split_rec = nullptr, *d_split_hand = nullptr;
-    int32_t *d_split_cnt = nullptr;
-    uint32_t *d_split_pix = nullptr;
-    size_t split_rec_bytes = 0;
-    uint32_t *d_split_count = nullptr;  // short launches (SCHED 5): the order kernel's split count
-    uint32_t *d_split_len = nullptr;    // SCHED 5: per tile (4 per block), where its rays stopped
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -618,7 +603,6 @@ struct Frame {
   bool degenerate = false;
   vr_context::Schedule *sched_copy = nullptr;  // a timed full-frame launch: copy its durations back
   vr_context::Schedule *sched = nullptr;       // the launch shape's schedule (attach_schedule)
-  bool split_short = false;  // a short launch may split its heaviest blocks in-workgroup (SCHED 5)
 };
 
 
@@ -860,12 +844,6 @@ void free_schedules(vr_context *h) {
     if (kv.second.h_cost) (void)hipHostFree(kv.second.h_cost);
     if (kv.second.h_order) (void)hipHostFree(kv.second.h_order);
     if (kv.second.copied) (void)hipEventDestroy(kv.second.copied);
-    vr_context::Schedule &S = kv.second;
-    for (void *q : {(void *)S.d_split_list, (void *)S.d_split_of, (void *)S.d_split_rec, (void *)S.d_split_hand,
-                    (void *)S.d_split_cnt, (void *)S.d_split_pix, (void *)S.d_split_count, (void *)S.d_split_len})
-      if (q) (void)hipFree(q);
-    for (void *q : {(void *)S.h_split_list, (void *)S.h_split_of})
-      if (q) (void)hipHostFree(q);
   }
   h->sched.clear();
 }
@@ -896,6 +874,9 @@ int device_wave_slots() {
 // restages.  Measured on MI355X (ms): tau 2.0 (C2, 1024x768, 3 rounds) K = 4 19.5, K = 2 29.8,
 // K = 8 25.1; tau 1.07 (metric, 7.9 rounds) K = 2 36.5, K = 4 37.6, K = 1 51.7; tau 1.0 (C5,
 // 4096^2, 64 rounds) K = 2 293.6, K = 4 338.5, K = 1 348.7.  K = 1 only for sparse sampling.
+#ifndef VR_COUNT_K
+#define VR_COUNT_K 0  // 1 (diagnostic build, as vr_march.hip): counter variants at every depth-lane count
+#endif
 #ifndef VR_XCD_RUN
 #define VR_XCD_RUN 0  // march workgroups -> XCD runs (vr_march.hip xcd_block); 0: dispatch order
 #endif
@@ -952,15 +933,6 @@ bool want_schedule(const vr::RenderParams &P) {
   return env_flag("VR_SCHED") || short_launch(P) || !env_flag_off("VR_SCHED_FULL");
 }
 
-std::vector<uint32_t> split_choose(const uint32_t *cost, uint32_t nb, uint32_t W);
-hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uint32_t nb,
-                        const std::vector<uint32_t> *chosen, hipStream_t stream);
-hipError_t split_records(vr_context::Schedule &S, const vr::RenderParams &P, uint32_t rays, hipStream_t stream);
-
-#ifndef VR_SPLIT_SHORT_NUM
-#define VR_SPLIT_SHORT_NUM 6  // in-workgroup split of a short launch: blocks >= 6/16 of the longest
-#endif
-
 // launch_order's tail argument: (tail_pct << 32) | resident workgroups; tail_pct 0 = heavy-first.
 uint64_t wg_tail_arg(uint32_t tail_pct) {
   return (uint64_t)tail_pct << 32 | (uint64_t)(device_wave_slots() / 16 * 6);
@@ -997,39 +969,11 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   const bool full = !short_launch(P) && !env_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
   if (!full) {  // short launch: every launch measured, ordered longest first by the previous one
     P.sched_full = 0;
-    // in-workgroup chord split (SCHED 5, F.split_short): the order kernel also counts the blocks to
-    // split (the leading ones lasting >= VR_SPLIT_SHORT_NUM / 16 of the longest, at most nb / 4)
-    uint32_t ns_cap = 0, num = VR_SPLIT_SHORT_NUM;
-    if (const char *ev = std::getenv("VR_SPLIT_SHORT_NUM")) num = (uint32_t)std::min(16, std::max(1, std::atoi(ev)));
-    if (F.split_short && nb >= 8) {
-      hipError_t e = S.d_split_count ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&S.d_split_count), sizeof(uint32_t));
-      if (e == hipSuccess && !S.d_split_len) {
-        e = hipMalloc(reinterpret_cast<void **>(&S.d_split_len), (size_t)nb * 4u * sizeof(uint32_t));
-        if (e == hipSuccess) e = hipMemsetAsync(S.d_split_len, 0, (size_t)nb * 4u * sizeof(uint32_t), stream);
-      }
-      if (e == hipSuccess) e = split_records(S, P, (nb / 4) * 4u * (64u / (uint32_t)K), stream);
-      if (e == hipSuccess) ns_cap = nb / 4;
-      else vr_host::consume(e, "split buffers (the short launch runs unsplit)");
-    }
     if (S.measured) {
-      // VR_SCHED_SHORT_DIV=d (A/B): the heavy blocks (>= 1/d of the longest) first, the rest row-major
-      uint32_t div = 0;
-      if (const char *ev = std::getenv("VR_SCHED_SHORT_DIV")) div = (uint32_t)std::max(0, std::atoi(ev));
-      if (ns_cap) div = 0;
-      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, div, div ? wg_tail_arg(0) : 0u,
-                            ns_cap ? S.d_split_count : nullptr, num, ns_cap);
+      rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, 0u, 0u);
     } else {  // first launch of this shape: row-major order, durations recorded
       rc = vr::launch_iota(S.d_order, nb, stream);
-      if (rc == hipSuccess && ns_cap) rc = hipMemsetAsync(S.d_split_count, 0, sizeof(uint32_t), stream);
       S.measured = true;
-    }
-    if (ns_cap) {
-      P.split_count = S.d_split_count;
-      P.split_len = env_flag("VR_SPLIT_CHORD") ? nullptr : S.d_split_len;  // (A/B: half the chord)
-      P.split_n = ns_cap;
-      P.split_rec = S.d_split_rec;
-      P.split_cap = S.split_cap;
-      P.split_thr = P.thr + 4e-3f < 1.f ? P.thr + 4e-3f : 2.f;
     }
   } else {
     // full frame: the block durations are measured on the first launch of the shape and every
@@ -1074,12 +1018,6 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
       S.tail = rows || shift > 0.0 || (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
       S.decided = true;
       S.order_stale = true;
-      // the chord split of the following unscheduled frames, chosen now: h_cost is rewritten by the
-      // next measurement's copy
-      if (env_flag("VR_SPLIT")) {
-        S.split_plan = split_choose(S.h_cost, nb, (uint32_t)(device_wave_slots() / 16 * 5));
-        S.split_stale = true;
-      }
       // workgroup wg is tile block (wg % nbx, wg / nbx) (vr_march.hip march_kernel)
       const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
       const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
@@ -1144,167 +1082,6 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   // none for a full frame, whose first blocks are only the heavy ones
   P.prio_blocks = P.sched_full ? 0u : (uint32_t)(device_wave_slots() / 4);
   if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
-  return hipSuccess;
-}
-
-// ---- chord split (DESIGN.md s8 "chord split"; vr_march.hip SCHED 4) ------------------------------
-// A block whose waves march rays crossing both shell walls lasts up to ten times the median and, in
-// row-major order, may start late and end alone (the frame's ramp-down).  Such a block is marched
-// twice at once: its front halves (A) in the block's own place and its back halves (B) among the
-// first workgroups of the launch; split_composite_kernel joins them in sample order afterwards --
-// bit-identical to one pass.
-#ifndef VR_SPLIT_MIN_FRAC
-#define VR_SPLIT_MIN_FRAC 0.10  // split only blocks lasting at least this fraction of the packed frame
-#endif
-#ifndef VR_SPLIT_GAIN
-#define VR_SPLIT_GAIN 0.97  // ... and only if the simulated frame shrinks below this fraction
-#endif
-
-// List scheduling of blocks with durations d in `order` over W workgroup slots (the dispatcher gives
-// the next block to the first free slot); per block its end time; returns the makespan.
-double sim_list(const std::vector<double> &d, const std::vector<uint32_t> &order, uint32_t W,
-                std::vector<double> *end) {
-  std::priority_queue<double, std::vector<double>, std::greater<double>> free_at;
-  for (uint32_t i = 0; i < W; ++i) free_at.push(0.0);
-  double span = 0.0;
-  for (uint32_t b : order) {
-    const double t0 = free_at.top();
-    free_at.pop();
-    const double t1 = t0 + d[b];
-    if (end) (*end)[b] = t1;
-    free_at.push(t1);
-    span = std::max(span, t1);
-  }
-  return span;
-}
-
-// The blocks to split, from the durations of the last measured launch (row-major order): those that
-// end after the packed frame (sum / W) in a simulation of the launch and last at least
-// VR_SPLIT_MIN_FRAC of it, over two rounds (a split moves the other blocks); none unless the
-// simulated split frame is shorter by VR_SPLIT_GAIN.  At most nb / 8 blocks.
-std::vector<uint32_t> split_choose(const uint32_t *cost, uint32_t nb, uint32_t W) {
-  std::vector<double> d(nb);
-  double sum = 0.0;
-  for (uint32_t i = 0; i < nb; ++i) sum += (d[i] = (double)cost[i]);
-  const double packed = sum / std::max<uint32_t>(W, 1u);
-  double min_frac = VR_SPLIT_MIN_FRAC, gain = VR_SPLIT_GAIN;  // (A/B: VR_SPLIT_MIN_FRAC, VR_SPLIT_GAIN)
-  if (const char *ev = std::getenv("VR_SPLIT_MIN_FRAC")) min_frac = std::atof(ev);
-  if (const char *ev = std::getenv("VR_SPLIT_GAIN")) gain = std::atof(ev);
-  std::vector<uint32_t> order(nb);
-  for (uint32_t i = 0; i < nb; ++i) order[i] = i;
-  std::vector<double> end(nb);
-  const double span0 = sim_list(d, order, W, &end);
-  std::vector<char> split(nb, 0);
-  std::vector<uint32_t> chosen;
-  double span = span0;
-  for (int round = 0; round < 2; ++round) {
-    for (uint32_t i = 0; i < nb && chosen.size() < nb / 8; ++i)
-      if (!split[i] && end[i] > packed && d[i] >= min_frac * packed) {
-        split[i] = 1;
-        chosen.push_back(i);
-      }
-    // the split launch: the back halves first, then every block in row-major order (halved if split)
-    std::vector<double> dd(d);
-    std::vector<uint32_t> ord2;
-    for (size_t j = 0; j < chosen.size(); ++j) {
-      dd.push_back(d[chosen[j]] * 0.5);
-      ord2.push_back(nb + (uint32_t)j);
-    }
-    for (uint32_t i = 0; i < nb; ++i) {
-      if (split[i]) dd[i] = d[i] * 0.5;
-      ord2.push_back(i);
-    }
-    std::vector<double> end2(dd.size());
-    span = sim_list(dd, ord2, W, &end2);
-    for (uint32_t i = 0; i < nb; ++i) end[i] = end2[i];
-  }
-  if (env_flag("VR_SPLIT_DEBUG"))  // diagnostics: the simulation behind the decision
-    std::fprintf(stderr, "split_choose: %u blocks, W %u, packed %.0f, row-major span %.0f, %zu split -> span %.0f\n",
-                 nb, W, packed, span0, chosen.size(), span);
-  if (chosen.empty() || span > gain * span0) chosen.clear();
-  return chosen;
-}
-
-// Fill S's split buffers for `chosen` (tile blocks of a K-lane launch of nb blocks; null: keep the
-// last plan) and attach them to P.  A split ray's records hold its back half: at most half the
-// longest chord of its wave in samples plus the drift of the t recurrence (t += tstep rounds by up
-// to ulp(t) / 2 per sample).
-// The records of `rays` split rays (their back halves' samples): at most half the longest chord of
-// a wave in samples plus the drift of the t recurrence (t += tstep rounds by up to ulp(t) / 2 per
-// sample) per ray; S.split_cap is set to that capacity.  Grown only (a launch in flight on this
-// stream may read the old buffers: waited for first).
-hipError_t split_records(vr_context::Schedule &S, const vr::RenderParams &P, uint32_t rays, hipStream_t stream) {
-  double pmax = 0.0, diag = 0.0;
-  for (int i = 0; i < 3; ++i) {
-    pmax = std::max(pmax, (double)std::fabs(P.eye[i]) + std::fabs(P.bmin[i]));
-    diag += 4.0 * (double)P.bmin[i] * P.bmin[i];
-  }
-  diag = std::sqrt(diag);
-  const double est = diag / (double)P.tstep + 2.0;
-  const double drift = est * std::ldexp(1.0, std::ilogb(pmax + diag) - 24) / (double)P.tstep;
-  const uint32_t cap = (uint32_t)std::min(est * 0.5 + drift + 64.0, (double)P.max_steps);
-  const size_t rec_bytes = (size_t)rays * cap * 4 * sizeof(float);
-  if (rays > S.split_slots || rec_bytes > S.split_rec_bytes) {
-    VR_HIP(hipStreamSynchronize(stream));
-    for (void *q : {(void *)S.d_split_rec, (void *)S.d_split_hand, (void *)S.d_split_cnt, (void *)S.d_split_pix})
-      if (q) (void)hipFree(q);
-    S.d_split_rec = S.d_split_hand = nullptr;
-    S.d_split_cnt = nullptr;
-    S.d_split_pix = nullptr;
-    S.split_slots = 0;
-    S.split_rec_bytes = 0;
-    S.split_n = 0;
-    const uint32_t rays_alloc = rays + rays / 4;
-    const size_t bytes = rec_bytes + rec_bytes / 4;
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&S.d_split_rec), bytes);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_hand), rays_alloc * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_cnt), rays_alloc * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_pix), rays_alloc * sizeof(uint32_t));
-    if (e != hipSuccess) return e;
-    S.split_slots = rays_alloc;
-    S.split_rec_bytes = bytes;
-  }
-  S.split_cap = cap;
-  return hipSuccess;
-}
-
-hipError_t split_attach(vr_context::Schedule &S, vr::RenderParams &P, int K, uint32_t nb,
-                        const std::vector<uint32_t> *chosen, hipStream_t stream) {
-  if (chosen) {  // a new plan
-    const uint32_t n = (uint32_t)chosen->size();
-    if (!S.d_split_of) {
-      hipError_t e = hipMalloc(reinterpret_cast<void **>(&S.d_split_of), nb * sizeof(int32_t));
-      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_split_of), nb * sizeof(int32_t));
-      if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.d_split_list), nb * sizeof(uint32_t));
-      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_split_list), nb * sizeof(uint32_t));
-      if (e != hipSuccess) return e;
-    }
-    const uint32_t rays = n * 4u * (64u / (uint32_t)K);
-    VR_HIP(split_records(S, P, rays, stream));
-    // the pinned plan buffers are rewritten only after their previous copy has run
-    VR_HIP(hipStreamSynchronize(stream));
-    for (uint32_t i = 0; i < nb; ++i) S.h_split_of[i] = -1;
-    for (uint32_t j = 0; j < n; ++j) {
-      S.h_split_list[j] = (*chosen)[j];
-      S.h_split_of[(*chosen)[j]] = (int32_t)j;
-    }
-    VR_HIP(hipMemcpyAsync(S.d_split_of, S.h_split_of, nb * sizeof(int32_t), hipMemcpyHostToDevice, stream));
-    if (n) VR_HIP(hipMemcpyAsync(S.d_split_list, S.h_split_list, n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-    S.split_n = n;
-    S.split_stale = false;
-  }
-  if (!S.split_n) return hipSuccess;
-  P.split_n = S.split_n;
-  P.split_list = S.d_split_list;
-  P.split_of = S.d_split_of;
-  P.split_rec = S.d_split_rec;
-  P.split_cnt = S.d_split_cnt;
-  P.split_pix = S.d_split_pix;
-  P.split_hand = S.d_split_hand;
-  P.split_cap = S.split_cap;
-  // B stops once its own opacity passes thr by more than the rounding of two fp32 recurrences can
-  // set it apart from the ray's true opacity (at least B's in exact arithmetic); never for thr near 1
-  P.split_thr = P.thr + 4e-3f < 1.f ? P.thr + 4e-3f : 2.f;
   return hipSuccess;
 }
 
@@ -1392,12 +1169,11 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const uint64_t n = bx->bytes / sizeof(float);
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
-      gv->bytes = n * (VR_GVEC_ZPAIR == 2 ? 3 : VR_GVEC_ZPAIR ? 8 : 4) * sizeof(float);
+      gv->bytes = n * 4 * sizeof(float);
       const hipError_t ea = vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device);
       if (ea == hipSuccess) {
         for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);
-        const uint64_t pxy = (bx->dims[0] + 2) * (bx->dims[1] + 2);
-        VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, pxy, stream));
+        VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
         // launches on other streams (another handle, a group's other children on this device) find
         // the copy fresh and wait for this event before reading it (bind_reads)
         VR_HIP(vr_host::record_event(stream, gv->ready));
@@ -1425,7 +1201,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   if (march) {
     // the counter variant: K = 1 (VR_COUNT_PROD=1 with a VR_COUNT_K=1 build: the production K's chunk
     // statistics; its sample sums are then 0)
-    const int K = (P.steps && !env_flag("VR_COUNT_PROD")) ? 1 : exact_lanes(depth_lanes(P), P.fast_shade);
+    // (VR_COUNT_PROD is honoured by a VR_COUNT_K build only: a normal build has no counted K > 1 kernel)
+    const int K = (P.steps && !(VR_COUNT_K && env_flag("VR_COUNT_PROD"))) ? 1
+                                                                          : exact_lanes(depth_lanes(P), P.fast_shade);
     set_chunk_halo(F, K);
     typedef hipError_t (*launch_fn)(const vr::RenderParams &, int, bool, bool, bool, hipStream_t);
     typedef uint32_t (*blocks_fn)(const vr::RenderParams &);
@@ -1437,36 +1215,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
          VR_K8(vr::fast::launch_march_k8, vr::fast::launch_march_k4)}};
     const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
     // (the exact-arithmetic variant is a parity reference: built without the scheduled kernels)
-    // chord split (split_choose; opt-in, VR_SPLIT=1 -- measured slower on MI355X): an
-    // unscheduled full frame whose last measured durations show blocks ending after the packed frame.
-    // VR_SPLIT_FORCE=f (tests): any eligible launch, unscheduled, with a pseudo-random fraction f of
-    // its blocks split (all: f >= 1)
-    const bool can_split = K > 1 && P.fast_shade && P.tame && F.mode >= 1 && F.ab_alias && !F.big && !P.wide_slot &&
-                           P.views <= 1 && !P.steps;
-    const char *force = can_split ? std::getenv("VR_SPLIT_FORCE") : nullptr;
-    // VR_SPLIT_SHORT=1: short launches (an image part of a multi-GPU frame) split their heaviest
-    // blocks inside the workgroup (SCHED 5)
-    F.split_short = can_split && env_flag("VR_SPLIT_SHORT");
-    if (force) {
-      static const blocks_fn fbf[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
-                                       VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
-      const uint32_t nb = fbf[ki](P);
-      char key[300];
-      std::snprintf(key, sizeof key, "split-force/%d/%d/%d/%d/%d/%u/%p", K, P.width, P.height, P.part, P.num_parts, nb,
-                    (void *)stream);
-      vr_context::Schedule &S = h->sched[key];
-      const double f = std::atof(force);
-      std::vector<uint32_t> ch;
-      for (uint32_t i = 0; i < nb; ++i)
-        if (f >= 1.0 || (double)((i * 2654435761u) >> 8 & 0xffffu) < f * 65536.0) ch.push_back(i);
-      VR_HIP(split_attach(S, P, K, nb, &ch, stream));
-    } else {
-      if (!P.steps && K > 1 && P.fast_shade && want_schedule(P)) VR_HIP(attach_schedule(h, P, F, K, stream, ""));
-      if (can_split && env_flag("VR_SPLIT") && !P.wg_order && F.sched && F.sched->decided && !F.sched->tail) {
-        vr_context::Schedule &S = *F.sched;
-        VR_HIP(split_attach(S, P, K, S.blocks, S.split_stale ? &S.split_plan : nullptr, stream));
-      }
-    }
+    // (scheduled kernels exist for absorption = emission only: vr_march.hip launch_c)
+    if (!P.steps && K > 1 && P.fast_shade && F.ab_alias && want_schedule(P))
+      VR_HIP(attach_schedule(h, P, F, K, stream, ""));
     if (P.views > 1) {
       static const blocks_fn vfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2,
                                         vr::fast::march_blocks_k4,
@@ -1480,14 +1231,6 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_start), (size_t)P.sched_blocks * 4);
       if (e == hipSuccess) P.wg_start = d_start;
       else vr_host::consume(e, "hipMalloc (VR_SCHED_DUMP start ticks; not recorded)");
-    }
-    uint32_t *d_sdbg = nullptr;  // (SCHED 5) per split tile: A's / B's march ticks, the split index
-    const size_t sdbg_n = (size_t)P.sched_blocks * 4u * 3u;
-    if (dump && P.split_count) {
-      hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_sdbg), sdbg_n * 4);
-      if (e == hipSuccess) e = hipMemsetAsync(d_sdbg, 0, sdbg_n * 4, stream);
-      if (e == hipSuccess) P.split_dbg = d_sdbg;
-      else vr_host::consume(e, "VR_SCHED_DUMP split ticks (not recorded)");
     }
     // VR_BLOCK_ROT_ROWS=r (A/B): the unscheduled launch starts at block row r of the row-major order
     // and wraps (the light top rows then fill the ramp-down of the heavy middle band)
@@ -1506,10 +1249,6 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const hipError_t e = fns[P.fast_shade ? 1 : 0][ki](P, F.mode, F.ab_alias, F.share, F.big, stream);
       if (e != hipSuccess) throw HipError{e, "the march kernel launch (launch_march_k)"};
     }
-    // SCHED 4 (a full frame's split): the split rays' back halves composited onto their front halves,
-    // in order (a short launch's in-workgroup split, SCHED 5, composites inside the march kernel)
-    if (P.split_n && !P.split_count)
-      VR_HIP(vr::launch_split_composite(P, P.split_n * 4u * (64u / (uint32_t)K), stream));
     time_mark(h, 1, stream);
     if (F.sched_copy) {  // a timed full frame: its block durations to the host, for the tail test
       vr_context::Schedule &S = *F.sched_copy;
@@ -1536,17 +1275,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
           std::fwrite(st.data(), 4, st.size(), f);
           std::fclose(f);
         }
-      if (P.split_dbg) {
-        std::vector<uint32_t> sd(sdbg_n);
-        VR_HIP(hipMemcpy(sd.data(), d_sdbg, sdbg_n * 4, hipMemcpyDeviceToHost));
-        if (FILE *f = std::fopen((std::string(dump) + ".split").c_str(), "ab")) {
-          std::fwrite(hdr, 4, 4, f);
-          std::fwrite(sd.data(), 4, sd.size(), f);
-          std::fclose(f);
-        }
-      }
     }
-    if (d_sdbg) (void)hipFree(d_sdbg);
   } else {
     VR_HIP(vr::launch_render(P, F.mode, F.ab_alias, F.big, F.share, stream));
     if (P.views > 1) {  // the general kernel renders one view per launch

@@ -5,15 +5,6 @@
 
 namespace vr {
 
-// Layout of the interleaved lookup gradient (RenderParams::gvec).  0 (default): (gx, gy, gz, 0) per
-// padded voxel.  1 (A/B, round 4): z-paired -- entry i is 32 bytes, voxel i and voxel i + pxy (the
-// next plane), so a lookup's eight corners lie in two 64-byte runs instead of four 32-byte runs;
-// measured slower (C3 37.7 vs 36.4 ms: twice the footprint), DESIGN.md s8.  2 (A/B): packed (gx, gy,
-// gz), 12 bytes per voxel -- measured slower as well (C3 37.7 vs 34.3 ms: smaller, unaligned loads).
-#ifndef VR_GVEC_ZPAIR
-#define VR_GVEC_ZPAIR 0
-#endif
-
 // A bound "texture": an fp32 volume resident in HBM in the apron layout of DESIGN.md s5 -- the
 // logical nx*ny*nz column-major volume (x fastest) surrounded by a one-voxel border that
 // replicates the edge voxels, i.e. P[k][j][i] = T[clamp(k-1)][clamp(j-1)][clamp(i-1)] for
@@ -66,7 +57,7 @@ struct RenderParams {
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
-  const float *gvec;              // lookup gradient interleaved (VR_GVEC_ZPAIR layout), or null
+  const float *gvec;              // lookup gradient interleaved, (gx, gy, gz, 0) per padded voxel, or null
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test
@@ -94,34 +85,12 @@ struct RenderParams {
   const uint32_t *wg_order;
   uint32_t *wg_cost;
   uint32_t *wg_start;             // diagnostics (VR_SCHED_DUMP): each timed block's start tick (low 32 bits)
-  uint32_t *split_dbg;            // diagnostics (VR_SCHED_DUMP, SCHED 5): per split tile, A's and B's
-                                  // march ticks and the split index
   uint32_t sched_blocks;          // length of wg_order / wg_cost (must equal the launch's grid)
   uint32_t sched_full;            // 0: a short launch's schedule (longest first, timed); full frames
                                   // (occupancy-capped kernel, heavy blocks first or row-major): 1 timed,
                                   // 2 following the last measured order without timing
   uint32_t prio_blocks;           // scheduled launch: the first prio_blocks workgroups (the longest)
                                   // run at raised wave priority
-  // chord split of the heaviest tile blocks (DESIGN.md s8 "chord split"; march_kernel SPLIT): the
-  // first split_n workgroups march the back halves of the blocks split_list[0 .. split_n) ("B":
-  // from sample index n_split on, each sample's premultiplied colour and opacity stored to
-  // split_rec, nothing composited into the image), the rest march the frame, the split blocks'
-  // rays only up to n_split ("A"); split_composite_kernel then composites each split ray's stored
-  // samples onto its A state in order, with the early exit -- the sequential loop's arithmetic.
-  // n_split is per wave: half the longest chord (in samples) of its rays, the same in A and B.
-  const uint32_t *split_list;     // B workgroup b -> tile block
-  const int32_t *split_of;        // tile block -> split slot (index into split_list), or -1
-  float *split_rec;               // per split ray (slot x wave x ray): split_cap records of 4 floats
-  int32_t *split_cnt;             // per split ray: records B stored (-1: no ray)
-  uint32_t *split_pix;            // per split ray: its output pixel index (B), or ~0
-  float *split_hand;              // per split ray: A's opacity when it handed over, or -1
-  uint32_t split_n, split_cap;     // split_n: the launch's extra workgroups (SCHED 4: the back halves;
-                                  // SCHED 5: the room for *split_count split blocks)
-  const uint32_t *split_count;    // SCHED 5 (in-workgroup split of a short launch): how many of the
-                                  // order's first blocks are split (written by the order kernel)
-  uint32_t *split_len;            // SCHED 5: per tile, the sample index its rays last needed (the
-                                  // previous launch's; 0 unknown) -- the split index is half of it
-  float split_thr;               // B's own stop: its local opacity past thr + margin
   unsigned long long *steps;      // optional sample counter
   // sort-last slab launch (vr_render_slab): owned normalized z range [slab_z0,
   // slab_z1), the margin of the chunk ownership test, the resident padded planes [slab_pk0,

@@ -387,59 +387,6 @@ hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, fl
   return hipGetLastError();
 }
 
-// Chord split (vr_march.hip SCHED 4, RenderParams::split_*): per split ray, its back half's stored
-// samples composited onto the front half's result in sample order -- the reference's loop body
-// (volumeRender_kernel.cu:476-486: sum += (1 - sum.a) * col, stop once sum.a > thr) on the values the
-// march computed; the records hold exactly the samples that exist (t <= tfar, under max_steps) and
-// the ones of empty-chunk leaps (which add exactly nothing) are left out.  One lane per ray, its
-// records streamed 8 at a time.  A record count of -2 (capacity exceeded; the host sizes the
-// buffer so that it cannot happen) marks the pixel NaN rather than leave it silently wrong.
-__global__ __launch_bounds__(256) void split_composite_kernel(const RenderParams P, uint32_t nrays) {
-  const uint32_t id = blockIdx.x * 256u + threadIdx.x;
-  if (id >= nrays) return;
-  const uint32_t pix = P.split_pix[id];
-  const float hand = P.split_hand[id];
-  const int cnt = P.split_cnt[id];
-  if (pix == 0xffffffffu || !(hand >= 0.f)) return;  // no ray, or its front half stopped it
-  const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
-  float *o = P.out + pix;
-  if (cnt < 0) {
-    o[0] = o[plane] = o[2 * plane] = __builtin_nanf("");
-    return;
-  }
-  float sr = o[0], sg = o[plane], sb = o[2 * plane], sa = hand;
-  const float4 *rec = reinterpret_cast<const float4 *>(P.split_rec) + (size_t)id * P.split_cap;
-  const float thr = P.thr;
-  for (int j0 = 0; j0 < cnt; j0 += 8) {
-    float4 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = j0 + i < cnt ? rec[j0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    bool stop = false;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (!stop && j0 + i < cnt) {
-        const float om = 1.f - sa;
-        sr = fmaf(om, v[i].x, sr);
-        sg = fmaf(om, v[i].y, sg);
-        sb = fmaf(om, v[i].z, sb);
-        sa = fmaf(om, v[i].w, sa);
-        stop = sa > thr;
-      }
-    }
-    if (stop) break;
-  }
-  o[0] = sr;
-  o[plane] = sg;
-  o[2 * plane] = sb;
-}
-
-hipError_t launch_split_composite(const RenderParams &P, uint32_t nrays, hipStream_t s) {
-  if (!nrays) return hipSuccess;
-  if (!P.split_pix || !P.split_hand || !P.split_cnt || !P.split_rec || P.split_count) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(split_composite_kernel, dim3((nrays + 255) / 256), dim3(256), 0, s, P, nrays);
-  return hipGetLastError();
-}
-
 __global__ __launch_bounds__(256) void interleave3_kernel(const float *__restrict__ a, const float *__restrict__ b,
                                                           const float *__restrict__ c, float4 *__restrict__ out,
                                                           uint64_t n) {
@@ -447,44 +394,15 @@ __global__ __launch_bounds__(256) void interleave3_kernel(const float *__restric
     out[i] = make_float4(a[i], b[i], c[i], 0.f);
 }
 
-// The z-paired interleave (VR_GVEC_ZPAIR): entry i = (a, b, c, 0) of voxel i, then of voxel i + pxy
-// (the last plane's second half repeats its first: no lookup reads it -- a cell's upper plane is at
-// most the apron plane, whose entries lie one plane below).
-__global__ __launch_bounds__(256) void interleave3z_kernel(const float *__restrict__ a, const float *__restrict__ b,
-                                                           const float *__restrict__ c, float4 *__restrict__ out,
-                                                           uint64_t n, uint64_t pxy) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t j = i + pxy < n ? i + pxy : i;
-    out[2 * i] = make_float4(a[i], b[i], c[i], 0.f);
-    out[2 * i + 1] = make_float4(a[j], b[j], c[j], 0.f);
-  }
-}
-
-// The packed interleave (VR_GVEC_ZPAIR 2): (a, b, c) of voxel i at floats 3i .. 3i + 2
-__global__ __launch_bounds__(256) void interleave3p_kernel(const float *__restrict__ a, const float *__restrict__ b,
-                                                           const float *__restrict__ c, float *__restrict__ out,
-                                                           uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    out[3 * i] = a[i];
-    out[3 * i + 1] = b[i];
-    out[3 * i + 2] = c[i];
-  }
-}
-
-// out: n entries of the VR_GVEC_ZPAIR layout (pxy: the plane pitch of the padded volume)
-hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n, uint64_t pxy,
+// out: n entries (gx, gy, gz, 0) of the interleaved lookup gradient (RenderParams::gvec).  (Round 4
+// also measured a z-paired and a packed 12-byte layout, both slower; removed in round 5.)
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n,
                               hipStream_t s) {
   if (!n) return hipSuccess;
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 262144) blocks = 262144;
-  if (VR_GVEC_ZPAIR == 2)
-    hipLaunchKernelGGL(interleave3p_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c, out, n);
-  else if (VR_GVEC_ZPAIR)
-    hipLaunchKernelGGL(interleave3z_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
-                       reinterpret_cast<float4 *>(out), n, pxy);
-  else
-    hipLaunchKernelGGL(interleave3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
-                       reinterpret_cast<float4 *>(out), n);
+  hipLaunchKernelGGL(interleave3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
+                     reinterpret_cast<float4 *>(out), n);
   return hipGetLastError();
 }
 
@@ -521,32 +439,20 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t c) {
   return min(255u, e * 8u + m);
 }
 
-// split_n (optional): how many blocks lead the order with a duration of at least split_num / 16 of
-// the longest one (whole buckets, at most split_cap): the blocks a chord-split short launch marches
-// in two halves (vr_march.hip SCHED 5).
 __global__ __launch_bounds__(1024) void order_kernel(const uint32_t *__restrict__ cost, uint32_t n,
-                                                     uint32_t *__restrict__ order, uint32_t *split_n,
-                                                     uint32_t split_num, uint32_t split_cap) {
+                                                     uint32_t *__restrict__ order) {
   __shared__ uint32_t hist[256];
-  __shared__ uint32_t cmax;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
-  if (threadIdx.x == 0) cmax = 0;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    atomicAdd(&hist[cost_bucket(cost[i])], 1u);
-    if (split_n) atomicMax(&cmax, cost[i]);
-  }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[cost_bucket(cost[i])], 1u);
   __syncthreads();
   if (threadIdx.x == 0) {  // exclusive offsets, largest bucket first
-    uint32_t acc = 0, heavy = 0;
-    const uint32_t tb = split_n ? cost_bucket((uint32_t)(((uint64_t)cmax * split_num) >> 4)) : 256u;
+    uint32_t acc = 0;
     for (int b = 255; b >= 0; --b) {
       const uint32_t c = hist[b];
       hist[b] = acc;
       acc += c;
-      if ((uint32_t)b >= tb) heavy = acc;
     }
-    if (split_n) *split_n = heavy < split_cap ? heavy : split_cap;
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[cost_bucket(cost[i])], 1u)] = i;
@@ -624,12 +530,12 @@ __global__ __launch_bounds__(1024) void order_heavy_kernel(const uint32_t *__res
 // heavy_div 0: longest first (short launches); else the full-frame order of order_heavy_kernel
 // with tail = (tail_pct << 32) | resident workgroups.
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s, uint32_t heavy_div,
-                        uint64_t tail, uint32_t *split_n, uint32_t split_num, uint32_t split_cap) {
+                        uint64_t tail) {
   if (!n) return hipSuccess;
   if (heavy_div)
     hipLaunchKernelGGL(order_heavy_kernel, dim3(1), dim3(1024), 0, s, cost, n, heavy_div, (uint32_t)(tail >> 32),
                        (uint32_t)tail, order);
-  else hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order, split_n, split_num, split_cap);
+  else hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
   return hipGetLastError();
 }
 

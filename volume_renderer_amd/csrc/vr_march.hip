@@ -336,8 +336,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
 // Front-to-back compositing of one sample and the march recurrences of volumeRender_kernel.cu:
 // 476-492, in the reference's order: early exit on sum.a > thr before t > tfar; pos += step only
 // while the ray goes on.
-// thr / cap: the exit threshold and the sample cap (P.thr / P.max_steps; a chord split's halves
-// use their own, march SPLIT).
+// thr / cap: the exit threshold and the sample cap (P.thr / P.max_steps).
 __device__ __forceinline__ void composite(const RenderParams &P, Ray &R, float r, float gg, float b, float alpha,
                                           float thr, int cap) {
   const float om = 1.f - R.sa;
@@ -434,33 +433,13 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // has the position, t and step count of the one-volume march.  A ray stops here when it
 // terminates, or at its first sample beyond the slab in its direction of travel (`past`), whose
 // state becomes the resume point (store_resume).
-// SPLIT (chord split, RenderParams::split_*): SR says the wave's role -- 0 the whole chord, 1 (A)
-// the samples below SR.n_split only, 2 (B) the samples from SR.n_split on, each stored to the ray's
-// records (SR.rec, compacted: the samples of empty-chunk leaps add exactly nothing and are not
-// stored) and composited locally only for B's own stop (opacity past P.split_thr); SR.wrote
-// returns the records this lane stored up to (B).
-// SCHED 5 (A and B waves of one workgroup): SR.stop points at the tile's per-ray flags in LDS --
-// A raises its ray's flag once the ray has stopped (opacity past thr), B reads it at each chunk
-// and drops the ray (its records would not be composited).
-struct SplitRole {
-  int role, n_split;
-  float *rec;  // this lane's ray's records (4 floats each)
-  int wrote;
-  volatile int *stop;  // SCHED 5: the tile's flags (nullptr otherwise)
-  int ray;             // this lane's ray in the tile
-};
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false,
-          bool SPLIT = false>
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
-                                      uint32_t kk = 0, SplitRole *SR = nullptr) {
+                                      uint32_t kk = 0) {
   static_assert(!COUNT || K == 1 || VR_COUNT_K, "the counter variant is built for K = 1 only (VR_COUNT_K: all K)");
   static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
-  static_assert(!SPLIT || (!SLAB && !COUNT), "chord split: not with slabs or counters");
-  // (wave-uniform) the sample cap and the exit threshold of this wave's role
-  const bool role_b = SPLIT && SR->role == 2;
-  const int cap = (SPLIT && SR->role == 1) ? min(SR->n_split, P.max_steps) : P.max_steps;
-  const float thr = role_b ? P.split_thr : P.thr;
-  int nrec = 0;  // B, K = 1: records stored (the compacted index of the next one)
+  const int cap = P.max_steps;
+  const float thr = P.thr;
   const float sbz = P.bmin[2], ssz = P.bscale[2];
   // slab mode: the ray has left the slab in its direction of travel (normalized z of its sample)
   auto beyond = [&](float zn) { return R.step.z >= 0.f ? zn >= P.slab_z1 : zn < P.slab_z0; };
@@ -468,15 +447,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   const int sub = lane & (K - 1);
   if constexpr (K > 1) {  // R.nsteps: 0, or the resume point's index (slab mode)
     R.mine = R.alive;
-    if (role_b)  // B: the recurrences of the first n_split samples replayed (exact), then this lane's
-      advance(P, SR->n_split + sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step);
-    else
-      leap(P, sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // to this lane's first sample
+    leap(P, sub, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // to this lane's first sample
     R.alive = group_any<K>(R.mine);
-  } else if (role_b) {
-    advance(P, SR->n_split, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step);
   }
-  int kb = 0;  // B, K > 1: compacted record index of this group's next iteration
 
   // VR_ADAPTIVE_S: the first box attempt of a chunk is twice the length the wave's last chunk
   // staged (its box grows little from one chunk to the next), and the shortest after a partial box,
@@ -493,10 +466,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   // VR_LIGHTS_HOIST: the first light pair likewise (shade_fast), when the frame has two or more
   DevLight pre2[2];
   const DevLight *pre = nullptr;
-  // (only where the registers fit without lowering occupancy or spilling: not K = 1, the slab, split
-  // or counter variants, nor the 64-bit, separate-absorption or full-gradient-tap ones)
-  if constexpr (!NANCHK && VR_LIGHTS_HOIST && MODE != 0 && K > 1 && AB_ALIAS && SHARE2 && !BIG && !SLAB &&
-                !SPLIT && !COUNT) {
+  // (only where the registers fit without lowering occupancy or spilling: not K = 1, the slab or
+  // counter variants, nor the 64-bit, separate-absorption or full-gradient-tap ones)
+  if constexpr (!NANCHK && VR_LIGHTS_HOIST && MODE != 0 && K > 1 && AB_ALIAS && SHARE2 && !BIG && !SLAB && !COUNT) {
     const bool two = P.num_lights >= 2;
     for (int j = 0; j < 2; ++j) {
       pre2[j] = two ? light_at(P, j) : DevLight{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -506,17 +478,6 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     if (two) pre = pre2;
   }
   while (__any(R.alive)) {
-    if constexpr (SPLIT) {
-      if (SR->stop) {  // SCHED 5: A publishes its stopped rays, B drops them (wave-uniform role)
-        if (SR->role == 1) {
-          if (sub == 0 && R.sa > thr) SR->stop[SR->ray] = 1;
-        } else if (role_b && SR->stop[SR->ray]) {
-          R.alive = false;
-          if constexpr (K > 1) R.mine = false;
-        }
-        if (!__any(R.alive)) break;
-      }
-    }
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
     int S;
     bool staged, partial;
@@ -617,10 +578,6 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
           R.nlit += shaded ? 1 : 0;
         }
-        if (role_b) {  // B: the sample's record, in sample order (past the capacity: -2, reported)
-          if (nrec < (int)P.split_cap) *reinterpret_cast<float4 *>(SR->rec + 4 * nrec) = make_float4(r, gg, b, alpha);
-          SR->wrote = ++nrec;
-        }
         composite(P, R, r, gg, b, alpha, thr, cap);
       }
     } else {
@@ -647,14 +604,6 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         if (COUNT) {
           ++C.iter;
           C.lit += (MODE != 0 && __any(shaded)) ? 1u : 0u;
-        }
-        if (role_b) {  // B: the group's existing samples (a prefix of its K) as records kb + sub
-          if (ex) {
-            if (kb + sub < (int)P.split_cap)
-              *reinterpret_cast<float4 *>(SR->rec + 4 * (kb + sub)) = make_float4(r, gg, b, alpha);
-            SR->wrote = kb + sub + 1;
-          }
-          kb += K;
         }
         composite_group<K, 0, VR_ZERO_FILL && !NANCHK && !SLAB>(P, R, ex ? 1.f : 0.f, r, gg, b, alpha, thr);
         if (SLAB && !inside) {
@@ -746,60 +695,20 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n, int run) {
 // instantiations: the hooks cost when compiled in, even unused).  SCHED 1: a short launch (few
 // rounds; uncapped registers, its longest waves share a SIMD with few others); 2: a full frame
 // (the occupancy cap of the unscheduled kernel); 3: a full frame following the order without
-// recording durations.
-// SCHED 4: a full frame in row-major order with the chord split of RenderParams::split_* (the
-// first split_n workgroups are the split blocks' back halves; split_composite_kernel follows).
-// SCHED 5: a short launch in longest-first order (as SCHED 1, timed) whose first *split_count blocks
-// are split inside their workgroups: each takes two workgroups, each of those two of its tiles, and a
-// tile's two waves march its front half (A, even wave) and back half (B, odd wave) at once; after a
-// workgroup barrier A composites B's records in order (DESIGN.md s9 "in-workgroup split").
+// recording durations.  (Round 4: two chord-split schedules, SCHED 4 / 5, measured slower and
+// removed in round 5 -- DESIGN.md s8, s9.)
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
-  constexpr bool TIMED = SCHED == 1 || SCHED == 2 || SCHED == 5;  // SCHED 3: the order only
-  constexpr bool SPLITW = SCHED == 5;
-  constexpr bool SPLIT = SCHED == 4 || SPLITW;
+  constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
-  SplitRole SR{0, 0, nullptr, 0, nullptr, 0};
-  int slot = -1;
-  uint32_t wgo;
-  int tile_in = wave;     // the tile of the block this wave marches
-  bool split_wg = false;  // SPLITW: this workgroup holds two split tiles of a block
-  int half = 0;
-  if constexpr (SPLITW) {
-    const uint32_t ns = *P.split_count;  // (uniform) written by the order kernel of this launch
-    uint32_t pos;
-    if (blockIdx.x < 2u * ns) {
-      pos = blockIdx.x >> 1;
-      half = (int)(blockIdx.x & 1u);
-      split_wg = true;
-      tile_in = (half << 1) | (wave >> 1);
-      SR.role = (wave & 1) ? 2 : 1;
-      slot = (int)((pos * 2u + (uint32_t)half) * 2u + (uint32_t)(wave >> 1));  // the tile's record slot
-    } else {
-      pos = blockIdx.x - ns;
-      if (pos >= P.sched_blocks) return;  // (whole workgroup) the grid's spare split capacity
-    }
-    wgo = P.wg_order[pos];
-  } else if constexpr (SPLIT) {
-    if (blockIdx.x < P.split_n) {  // a back half (B)
-      slot = (int)blockIdx.x;
-      wgo = P.split_list[slot];
-      SR.role = 2;
-    } else {
-      wgo = blockIdx.x - P.split_n;
-      slot = P.split_of[wgo];
-      SR.role = slot >= 0 ? 1 : 0;
-    }
-  } else {
-    wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
-    if (!SCHED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
-      wgo += P.block_rot;
-      if (wgo >= gridDim.x) wgo -= gridDim.x;
-    }
+  uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
+  if (!SCHED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
+    wgo += P.block_rot;
+    if (wgo >= gridDim.x) wgo -= gridDim.x;
   }
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
   if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
@@ -807,7 +716,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   const int view = (P.views > 1 && wgo >= P.view_blocks) ? 1 : 0;
   const uint32_t wg = view ? wgo - P.view_blocks : wgo;
   float *const out = view ? P.out2 : P.out;
-  const int tile = (int)wg * VR_WG_WAVES + tile_in;
+  const int tile = (int)wg * VR_WG_WAVES + wave;
   const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
   const int blk = tile >> 2, quad = tile & 3;
   const int ray = lane >> TS::LK;
@@ -834,136 +743,24 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
     R.t = tnear;
   }
-  // chord split: n_split = half the longest chord of the wave's rays in samples (wave-uniform; the
-  // same in the block's two halves, which set up the same rays); this lane's ray's records
-  const size_t rslot = SPLITW ? ((size_t)slot * (64 / K) + (size_t)ray)
-                              : SPLIT ? ((size_t)(slot * VR_WG_WAVES + wave) * (64 / K) + (size_t)ray) : 0;
-  // SCHED 5: the tile's flags (A's stopped rays, for B) in LDS, cleared before either wave starts
-  if constexpr (SPLITW) {
-    __shared__ int split_stop_lds[2][64];
-    if (split_wg) {  // (whole workgroup)
-      if (threadIdx.x < 128) split_stop_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
-      __syncthreads();
-      SR.stop = split_stop_lds[wave >> 1];
-      SR.ray = ray;
-    }
-  }
-  if (SPLIT && SR.role) {
-    const int est = R.alive ? (int)fminf((R.tfar - R.t) / P.tstep, 1.0e9f) : 0;
-    const int emax = wave_max(est);
-    SR.n_split = emax >> 1;
-    if (SPLITW && P.split_len) {
-      // SCHED 5: half the samples the tile's rays needed in the previous launch (where they stopped),
-      // so that A and B share the work actually done rather than the chord; B's part kept within
-      // the record capacity (split_records: half the longest chord + drift + 64)
-      const int used = (int)P.split_len[tile];  // (wave-uniform; A and B read the same entry)
-      if (used > 0) SR.n_split = max(used >> 1, emax - ((int)P.split_cap - 64));
-    }
-    SR.rec = P.split_rec + rslot * (size_t)P.split_cap * 4u;
-    if (SR.n_split < 1) {  // nothing to split in this wave: A marches it whole, B stores nothing
-      if (SR.role == 2) R.alive = false;
-      SR.role = SR.role == 1 ? 0 : 2;
-    }
-  }
-  if constexpr (SPLIT) {
-    if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP, false, true>(P, L, lane, R, C, 0u, &SR);
-    else
-      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP, false, true>(P, L, lane, R, C, 0u, &SR);
-  } else {
-    // every coordinate the march forms from a finite start and step is finite; a tame launch takes
-    // the fast path (sample_at: TAME)
-    if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
-    else
-      march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
-  }
+  // every coordinate the march forms from a finite start and step is finite; a tame launch takes
+  // the fast path (sample_at: TAME)
+  if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
+  else
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
-  if constexpr (SPLITW) {
-    if (split_wg && P.split_dbg && lane == 0) {  // diagnostics: this wave's march ticks
-      const size_t q = ((size_t)wg * VR_WG_WAVES + (size_t)tile_in) * 3u;
-      P.split_dbg[q + (SR.role == 2 ? 1 : 0)] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - clk0);
-      if (SR.role != 2) P.split_dbg[q + 2] = (uint32_t)SR.n_split;
-    }
-    // A's rays that stopped in its last chunk (B reads the flags at its chunk boundaries)
-    if (SR.stop && SR.role == 1 && (lane & (K - 1)) == 0 && R.sa > P.thr) SR.stop[ray] = 1;
-    if (split_wg) {  // (whole workgroup)
-      // B hands its record count to A through LDS; the barrier also orders B's record stores before
-      // A's loads (one workgroup, one CU)
-      __shared__ int split_cnt_lds[2][64];
-      __shared__ int split_end_lds[2][64];  // B: the sample index its ray stopped at
-      if (SR.role == 2) {  // (wave-uniform: every lane of a group joins the DPP moves)
-        const int n = group_max_i<K>(SR.wrote, SR.wrote);
-        const int e = group_max_i<K>(R.nsteps, R.nsteps);
-        if ((lane & (K - 1)) == 0) {
-          split_cnt_lds[wave >> 1][ray] = n <= (int)P.split_cap ? n : -2;
-          split_end_lds[wave >> 1][ray] = e;
-        }
-      }
-      __syncthreads();
-      if (SR.role == 1 && P.split_len) {
-        // the samples this tile's rays needed: where A stopped them (before its cap), else where B did
-        const int a = group_max_i<K>(R.nsteps, R.nsteps);
-        const int used = !active ? 0 : a < SR.n_split ? a : split_end_lds[wave >> 1][ray];
-        const int m = wave_max(used);
-        if (lane == 0) P.split_len[tile] = (uint32_t)m;
-      }
-      if (SR.role == 1) {
-        // A: B's samples composited in order onto the front half (the reference's loop body, the
-        // early exit after each sample), K records per group iteration, 8 iterations' loads in flight
-        const int cnt = split_cnt_lds[wave >> 1][ray];
-        const int sub = lane & (K - 1);
-        if (cnt < 0 && active && !(R.sa > P.thr))  // (capacity exceeded where needed: cannot happen, loud)
-          R.sr = R.sg = R.sb = __builtin_nanf("");
-        R.alive = active && cnt > 0 && !(R.sa > P.thr);
-        const float4 *rec = reinterpret_cast<const float4 *>(SR.rec);
-        for (int j = 0; __any(R.alive); j += 8 * K) {
-          float4 v[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int q = j + i * K + sub;
-            v[i] = (R.alive && q < cnt) ? rec[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (R.alive) composite_group<K, 0>(P, R, (j + i * K + sub < cnt) ? 1.f : 0.f, v[i].x, v[i].y, v[i].z,
-                                               v[i].w, P.thr);
-          if (j + 8 * K >= cnt) R.alive = false;
-        }
-      }
-    }
-    if (SR.role == 0 && P.split_len) {  // a tile marched whole: where its rays stopped
-      const int a = group_max_i<K>(R.nsteps, R.nsteps);
-      const int m = wave_max(active ? a : 0);
-      if (lane == 0) P.split_len[tile] = (uint32_t)m;
-    }
-  }
-  if (SPLITW && SR.role == 2) {
-    // B: nothing to store (A wrote the pixel)
-  } else if (SPLIT && !SPLITW && SR.role == 2) {
-    // B: how many records this ray's lanes stored (the group's largest), and its pixel
-    const int n = group_max_i<K>(SR.wrote, SR.wrote);
-    if ((lane & (K - 1)) == 0) {
-      P.split_cnt[rslot] = active ? (n <= (int)P.split_cap ? n : -2) : -1;
-      P.split_pix[rslot] = active ? (uint32_t)((size_t)lc * (size_t)P.height + (size_t)y) : 0xffffffffu;
-    }
-  } else if (active && (lane & (K - 1)) == 0) {
+  if (active && (lane & (K - 1)) == 0) {
     const size_t plane = (size_t)P.plane_cols * (size_t)P.height;
     const size_t kk = (size_t)lc * (size_t)P.height + (size_t)y;
     out[kk] = R.sr;
     out[kk + plane] = R.sg;
     out[kk + 2 * plane] = R.sb;
-    // A: the opacity to continue from when the ray did not stop (the reference goes on while
-    // !(sum.a > thr)); -1: stopped, nothing to add
-    if (SPLIT && !SPLITW && slot >= 0) P.split_hand[rslot] = (SR.role == 1 && !(R.sa > P.thr)) ? R.sa : -1.f;
   }
   if (TIMED) {  // this block's duration, for the next launch's schedule
     __syncthreads();
-    if (threadIdx.x == 0 && half == 0) {
-      // (a split block: its first workgroup's duration doubled -- what the block would last unsplit,
-      // so that the next launch splits it again rather than taking it for a light block)
-      uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
-      if (split_wg) d *= 2u;
+    if (threadIdx.x == 0) {
+      const uint64_t d = __builtin_amdgcn_s_memrealtime() - clk0;
       P.wg_cost[wgo] = d > 0xffffffffull ? 0xffffffffu : (uint32_t)d;
       if (P.wg_start) P.wg_start[wgo] = (uint32_t)clk0;
     }
@@ -1222,16 +1019,6 @@ hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mo
 #endif
 
 #if !VR_ISA_PROBE
-// Diagnostics (VR_LDS_PAD=bytes): unused dynamic LDS per workgroup of a short scheduled launch,
-// to cap the workgroups a CU holds (the heavy waves' co-residency).
-static unsigned short_launch_lds_pad() {
-  static const unsigned pad = [] {
-    const char *ev = getenv("VR_LDS_PAD");
-    return ev ? (unsigned)std::max(0, atoi(ev)) : 0u;
-  }();
-  return pad;
-}
-
 // VR_INJECT_BAD_LAUNCH=1 (tests only): the march launch asks for 2048 work-items per workgroup, more
 // than a gfx950 workgroup holds, so the runtime rejects it before dispatch -- the reporting path of
 // a failed launch (tests/test_gpu_streams.py::test_failed_launch_is_reported_by_its_call).  Read
@@ -1246,45 +1033,39 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   constexpr int K = VR_MARCH_K;
   const dim3 blk(inject_bad_launch() ? 2048 : 64 * VR_WG_WAVES);
   const bool sched = P.wg_order && P.wg_cost;
-  // scheduled kernels: K > 1, fast variant only (otherwise the names below alias the SCHED 0 kernel)
-  constexpr bool SCH = K > 1 && VR_MARCH_FAST;
+  // scheduled kernels: K > 1, fast variant, absorption = emission only (otherwise the names below
+  // alias the SCHED 0 kernel; the host schedules no other launch, vr_capi.hip attach_schedule)
+  constexpr bool SCH = K > 1 && VR_MARCH_FAST && AB;
   constexpr int S1 = SCH ? 1 : 0, S2 = SCH ? 2 : 0, S3 = SCH ? 3 : 0;
-  // the chord-split kernel (SCHED 4) only where the host splits: lit, absorption = emission, the
-  // default slot (vr_capi.hip split_plan)
-  constexpr bool SPL = SCH && AB && MODE >= 1 && CAP == VR_LDS_CAP;
-  constexpr int S4 = SPL ? 4 : 0, S5 = SPL ? 5 : 0;
-#define VR_LAUNCH(KK, CNT, BG, SC, PAD)                                                                    \
+#define VR_LAUNCH(KK, CNT, BG, SC)                                                                         \
   do {                                                                                                    \
-    hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, PAD, s, P);        \
+    hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, 0, s, P);          \
     note_march_kernel(VR_MARCH_FAST, KK, MODE, AB, CNT, SH, BG, CAP, SC);                                 \
   } while (0)
-  if (K == 1 && P.steps) {
-    if (big) VR_LAUNCH(1, true, true, 0, 0);
-    else VR_LAUNCH(1, true, false, 0, 0);
-  } else if (VR_COUNT_K && P.steps) {  // diagnostic build: chunk statistics at the production K
-    if (big) VR_LAUNCH(K, VR_COUNT_K != 0, true, 0, 0);
-    else VR_LAUNCH(K, VR_COUNT_K != 0, false, 0, 0);
-  } else if (!VR_MARCH_FAST && sched) {  // the exact variant is built without the scheduled kernels
+  // (the counter variant: instantiated in the K = 1 object only -- or at every K in a VR_COUNT_K build)
+  if constexpr (K == 1 || VR_COUNT_K) {
+    if (P.steps) {
+      if (big) VR_LAUNCH(K, true, true, 0);
+      else VR_LAUNCH(K, true, false, 0);
+      return hipGetLastError();
+    }
+  }
+  if (P.steps) {
     return hipErrorInvalidValue;
-  } else if (P.split_n && P.split_count) {  // a short launch, its heaviest blocks split in-workgroup
-    if (!SPL || big || !sched || P.sched_full) return hipErrorInvalidValue;
-    VR_LAUNCH(K, false, false, S5, short_launch_lds_pad());
-  } else if (P.split_n) {  // a full frame with its heaviest blocks split (not scheduled, 32-bit)
-    if (!SPL || big || sched) return hipErrorInvalidValue;
-    VR_LAUNCH(K, false, false, S4, 0);
+  } else if (sched && !SCH) {  // the exact variant and separate absorption have no scheduled kernels
+    return hipErrorInvalidValue;
   } else if (K > 1 && sched && P.sched_full == 1) {  // a full frame, durations measured
-    if (big) VR_LAUNCH(K, false, true, S2, 0);
-    else VR_LAUNCH(K, false, false, S2, 0);
+    if (big) VR_LAUNCH(K, false, true, S2);
+    else VR_LAUNCH(K, false, false, S2);
   } else if (K > 1 && sched && P.sched_full == 2) {  // a full frame in the last measured order
-    if (big) VR_LAUNCH(K, false, true, S3, 0);
-    else VR_LAUNCH(K, false, false, S3, 0);
+    if (big) VR_LAUNCH(K, false, true, S3);
+    else VR_LAUNCH(K, false, false, S3);
   } else if (K > 1 && sched) {  // a short launch (few waves per slot), longest first
-    const unsigned pad = short_launch_lds_pad();
-    if (big) VR_LAUNCH(K, false, true, S1, pad);
-    else VR_LAUNCH(K, false, false, S1, pad);
+    if (big) VR_LAUNCH(K, false, true, S1);
+    else VR_LAUNCH(K, false, false, S1);
   } else {
-    if (big) VR_LAUNCH(K, false, true, 0, 0);
-    else VR_LAUNCH(K, false, false, 0, 0);
+    if (big) VR_LAUNCH(K, false, true, 0);
+    else VR_LAUNCH(K, false, false, 0);
   }
 #undef VR_LAUNCH
   return hipGetLastError();
@@ -1318,11 +1099,8 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
   if (P.views > 1 && (P.view_blocks != per_view || !P.out2)) return hipErrorInvalidValue;
-  if (P.split_n && (P.views > 1 || VR_MARCH_K == 1 || !P.split_rec ||
-                    (P.split_count ? !P.wg_order : (!P.split_list || !P.split_of))))
-    return hipErrorInvalidValue;
-  const dim3 grid(per_view * (P.views > 1 ? 2u : 1u) + P.split_n);  // (split: the back halves first)
-  if (P.wg_order && (P.sched_blocks != grid.x - P.split_n || !P.wg_cost || VR_MARCH_K == 1))
+  const dim3 grid(per_view * (P.views > 1 ? 2u : 1u));
+  if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || VR_MARCH_K == 1))
     return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {
     case 0: return ab_alias ? launch_m<0, true, false>(P, grid, s, big) : launch_m<0, false, false>(P, grid, s, big);

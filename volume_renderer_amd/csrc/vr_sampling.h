@@ -274,29 +274,9 @@ __device__ __forceinline__ f3 fetch_vec(const float *gvec, const DevTex &t, cons
   uint64_t o;
   if (BIG) o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
   else o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
-#if VR_GVEC_ZPAIR == 2
-  // packed (gx, gy, gz) per voxel, 12 bytes (vr_device.h): a row pair of the lookup is 24 contiguous bytes
-  struct G6 {
-    float v[6];
-  };
-  const float *g0 = gvec + 3 * o;
-  const G6 r00 = *reinterpret_cast<const G6 *>(g0), r10 = *reinterpret_cast<const G6 *>(g0 + 3 * (uint64_t)t.px);
-  const G6 r01 = *reinterpret_cast<const G6 *>(g0 + 3 * (uint64_t)t.pxy);
-  const G6 r11 = *reinterpret_cast<const G6 *>(g0 + 3 * ((uint64_t)t.pxy + t.px));
-  const float4 a00 = make_float4(r00.v[0], r00.v[1], r00.v[2], 0.f), b00 = make_float4(r00.v[3], r00.v[4], r00.v[5], 0.f);
-  const float4 a10 = make_float4(r10.v[0], r10.v[1], r10.v[2], 0.f), b10 = make_float4(r10.v[3], r10.v[4], r10.v[5], 0.f);
-  const float4 a01 = make_float4(r01.v[0], r01.v[1], r01.v[2], 0.f), b01 = make_float4(r01.v[3], r01.v[4], r01.v[5], 0.f);
-  const float4 a11 = make_float4(r11.v[0], r11.v[1], r11.v[2], 0.f), b11 = make_float4(r11.v[3], r11.v[4], r11.v[5], 0.f);
-#elif VR_GVEC_ZPAIR
-  // z-paired entries (vr_device.h): entry e holds voxel e (float4 2e) and voxel e + pxy (2e + 1)
-  const float4 *b = reinterpret_cast<const float4 *>(gvec) + 2 * (uint64_t)o;
-  const float4 a00 = b[0], a01 = b[1], b00 = b[2], b01 = b[3];
-  const float4 a10 = b[2 * t.px], a11 = b[2 * t.px + 1], b10 = b[2 * t.px + 2], b11 = b[2 * t.px + 3];
-#else
   const float4 *b = reinterpret_cast<const float4 *>(gvec) + o;
   const float4 a00 = b[0], b00 = b[1], a10 = b[t.px], b10 = b[t.px + 1];
   const float4 a01 = b[t.pxy], b01 = b[t.pxy + 1], a11 = b[t.pxy + t.px], b11 = b[t.pxy + t.px + 1];
-#endif
   f3 r;
 #define VR_TRI(c)                                                                                  \
   {                                                                                                \

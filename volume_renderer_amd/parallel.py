@@ -38,6 +38,58 @@ def gather_partitions(local, gathered, world: int, rank: int, group=None) -> Non
     dist.gather(local, list(gathered.chunk(world)) if rank == 0 else None, dst=0, group=group)
 
 
+def volume_checksum(vol):
+    """An order-sensitive checksum of a volume's bytes (int64, device-side for a GPU tensor): the sum of
+    its 32-bit words weighted by their index mod 65521, plus their plain sum -- equal on two replicas
+    iff (with overwhelming probability) their bytes are."""
+    import torch
+    flat = vol.reshape(-1).view(torch.int32)
+    acc = torch.zeros(2, dtype=torch.int64, device=flat.device)
+    step = 1 << 26  # chunks: the int64 temporaries stay at 1.5 GiB whatever the volume
+    for i0 in range(0, flat.numel(), step):
+        w = flat[i0:i0 + step].to(torch.int64)
+        idx = torch.arange(i0, i0 + w.numel(), device=w.device, dtype=torch.int64) % 65521 + 1
+        acc[0] += (w * idx).sum()
+        acc[1] += w.sum()
+    return acc
+
+
+def broadcast_volume(vol, world: int, rank: int, src: int = 0, group=None) -> dict:
+    """The one-time volume distribution of SURVEY.md 8e ("Collectives"): the volume, resident on rank
+    `src` (uploaded or generated there), broadcast in place into every rank's replica buffer (RCCL
+    over xGMI on the GPU; gloo in the CPU test).  Timed with the backend's own completion (device
+    synchronise around it on a GPU), reported apart from the per-frame time; each replica's checksum
+    is all-gathered so that rank 0 can state that every rank holds the same bytes."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    nbytes = vol.numel() * vol.element_size()
+    if world == 1:
+        return {"bytes": int(nbytes), "ms": 0.0, "gb_per_s": None, "ranks": 1, "replicas_identical": True}
+    cuda = vol.is_cuda
+    if cuda:
+        torch.cuda.synchronize(vol.device)
+    dist.barrier(group=group)
+    t0 = time.perf_counter()
+    dist.broadcast(vol, src=src, group=group)
+    if cuda:
+        torch.cuda.synchronize(vol.device)
+    dist.barrier(group=group)
+    ms = (time.perf_counter() - t0) * 1e3
+    mine = volume_checksum(vol)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine, group=group)
+    same = all(bool(torch.equal(a, allv[src])) for a in allv)
+    t = torch.tensor([ms], dtype=torch.float64, device=vol.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    ms = float(t.item())
+    return {"bytes": int(nbytes), "ms": round(ms, 3), "gb_per_s": round(nbytes / ms / 1e6, 2) if ms > 0 else None,
+            "ranks": world, "replicas_identical": same, "backend": str(dist.get_backend(group)),
+            "what": "one-time dist.broadcast of the volume from rank %d (barrier to barrier, max over ranks); "
+                    "not part of the per-frame time" % src}
+
+
 def rank_report(kernel_ms: float, gather_ms: float, world: int, rank: int, device=None, group=None):
     """Per-rank attribution of a multi-GPU frame (bench.py at N > 1): every rank's mean march-kernel
     time (HIP events around its launch) and its gather + assembly time (from the end of its launch

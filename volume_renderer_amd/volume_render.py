@@ -49,6 +49,16 @@ _VOLUME_PROPS = ("VolumeEmission", "VolumeAbsorption", "VolumeReflection", "Volu
                  "VolumeGradientY", "VolumeGradientZ", "VolumeIllumination")
 
 
+def stereo_geometry(camera_x_offset, focal_length, image_resolution):
+    """VolumeRender.m:278-283 (render, CameraXOffset ~= 0): the eyes' offset `base`, the crop `delta`
+    (from ImageResolution(2), the image height) and the per-eye render resolution [H, W + delta]."""
+    base = camera_x_offset / 2
+    fov = 2 * math.atan(1 / focal_length)
+    delta = base * image_resolution[1] / (2 * focal_length * math.tan(fov / 2))
+    delta = int(math.floor(abs(delta) + 0.5)) * (1 if delta >= 0 else -1)  # MATLAB round
+    return base, delta, np.flip(np.asarray(image_resolution)) + np.array([0, delta])
+
+
 class VolumeRender:
     """Renderer handle; see VolumeRender.m:1-62 for the property documentation."""
 
@@ -153,11 +163,7 @@ class VolumeRender:
 
     def _stereo_geometry(self):
         """VolumeRender.m:278-283: (base, delta, resolution [H W+delta]) of the stereo pair."""
-        base = self.CameraXOffset / 2
-        fov = 2 * math.atan(1 / self.FocalLength)
-        delta = base * self.ImageResolution[1] / (2 * self.FocalLength * math.tan(fov / 2))
-        delta = int(math.floor(abs(delta) + 0.5)) * (1 if delta >= 0 else -1)  # MATLAB round
-        return base, delta, np.flip(self.ImageResolution) + np.array([0, delta])
+        return stereo_geometry(self.CameraXOffset, self.FocalLength, self.ImageResolution)
 
     def render(self) -> np.ndarray:
         """VolumeRender.m:264-309: mono render, or off-axis stereo composed from two renders."""
