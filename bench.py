@@ -161,6 +161,7 @@ def main():
     wave_stats = [int(v) for v in steps_t[5:7].tolist()]
     fail_hist = [int(v) for v in steps_t[8:40].tolist()]
     staged_by_s = [int(v) for v in steps_t[40:44].tolist()]
+    probe_stats = [int(steps_t[7].item()), int(steps_t[44].item())]
     prod_stats = None
     if args.chunk_stats_k:  # the same counted launch at the production K (vr_capi.hip VR_COUNT_PROD)
         steps_t.zero_()
@@ -325,6 +326,7 @@ def main():
             "wave_iterations_total_lit": wave_stats,
             "global_chunk_box_hist_256": fail_hist,
             "staged_chunks_by_S_32_16_8_4": staged_by_s,
+            "probe_runs_leaped_failed": probe_stats,
             "gb_per_s_sample_stream": round(4.0 * total_samples * F / (elapsed / args.steps) / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

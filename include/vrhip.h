@@ -140,6 +140,13 @@ uint64_t vr_timestamp(void);
  * vr_render writes it, bit-identical to the two separate renders. */
 int vr_render_stereo(vr_context *h, const vr_render_args *args, float base, float *out_left, float *out_right);
 
+/* vr_render_stereo into device memory on `stream` (asynchronous, as vr_render_device; one-device
+ * handles; d_steps as vr_render_device's, over both eyes).  VR_STEREO_PAIR=1 marches the pair with
+ * paired tiles (a wave holds the right eye's column c and the left eye's column
+ * c + shift, one staged box for both) -- a measurement switch, images bit-identical. */
+int vr_render_stereo_device(vr_context *h, const vr_render_args *args, float base, float *d_left, float *d_right,
+                            unsigned long long *d_steps, void *stream);
+
 /* Multi-channel frame (replaces the per-channel loops of examples/example3.m:
  * 61-233 -- sync a channel's volumes, render, next channel -- and the sum at example3.m:239).  A
  * channel is one VolumeRender object: its handle (distinct per channel), the arguments of its

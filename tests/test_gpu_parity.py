@@ -615,6 +615,36 @@ def test_fused_stereo_equals_two_renders(monkeypatch, counter_clock, lit):
     r.delete()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", ["2", "4"])
+def test_paired_stereo_tiles_equal_two_renders(monkeypatch, counter_clock, k):
+    """Fused stereo with paired tiles (VR_STEREO_PAIR=1, vr_march.hip SCHED 4): each wave
+    marches half a tile of each eye -- the right eye's column c with the left eye's c + shift -- and
+    stages one box for both.  Every pixel of both eyes is marched once with its own arithmetic, so
+    the pair is bit for bit the reference's two renders, for the converging shift and others
+    (none, odd, wider than the image)."""
+    from volume_renderer_amd import mex
+    monkeypatch.setenv("VR_DEPTH_LANES", k)
+    v = vr.Volume(O.shell_volume(64))  # a power-of-two cube: the half-texel tap launch
+    r = ex1_renderer(v, res=(90, 70), lights=True)
+    r.CameraXOffset = 0.5
+    monkeypatch.setenv("VR_NO_FUSED_STEREO", "1")
+    two = np.asarray(r.render(), np.float32)
+    monkeypatch.delenv("VR_NO_FUSED_STEREO")
+    monkeypatch.setenv("VR_FUSED_STEREO", "1")
+    monkeypatch.setenv("VR_STEREO_PAIR", "1")
+    assert two.max() > 0
+    for shift in (None, "1", "4", "13", "200"):
+        if shift is None:
+            monkeypatch.delenv("VR_STEREO_PAIR_SHIFT", raising=False)
+        else:
+            monkeypatch.setenv("VR_STEREO_PAIR_SHIFT", shift)
+        img = np.asarray(r.render(), np.float32)
+        assert mex.last_march_kernel().endswith(", 4>"), (shift, mex.last_march_kernel())
+        assert np.array_equal(img.view(np.uint32), two.view(np.uint32)), (k, shift)
+    r.delete()
+
+
 def _channel_pair(lit):
     """Two channels of an examples/example3.m-style frame: the main channel (V_shell) and a
     structure channel (a second field) with their own colour and factors, one object each."""

@@ -79,6 +79,8 @@ SIGNATURES = [
     ("vr_timestamp", c_uint64, []),
     ("vr_render_device", c_int, [c_void_p, POINTER(VrRenderArgs), POINTER(VrPartition), c_void_p, c_void_p,
                                  c_void_p]),
+    ("vr_render_stereo_device", c_int, [c_void_p, POINTER(VrRenderArgs), c_float, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
     ("vr_partition_columns", c_int64, [c_int64, POINTER(VrPartition)]),
     ("vr_assemble_partitions", c_int, [c_void_p, c_int64, c_int64, c_int32, c_int32, c_int64, c_void_p,
                                        c_void_p]),

@@ -75,6 +75,7 @@ hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
+hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, hipStream_t s);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n,
                               hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
@@ -217,8 +218,13 @@ struct DevBuf {
   // from which the fast shading's lookups take two 16-byte loads per light instead of four 8-byte
   float *zpair = nullptr;
   uint64_t zpair_bytes = 0;
+  // occupancy map (volumes of at least VR_OCC_MIN_VOXELS padded voxels; vr_kernels.hip
+  // occupancy_kernel): one byte per 8^3 brick, read by the march's empty-space probe
+  uint8_t *occ = nullptr;
+  uint64_t occ_bytes = 0;
   ~DevBuf() {
     if (zpair) vr_host::pooled_free(zpair, zpair_bytes, device, vr_host::Readers(readers));
+    if (occ) vr_host::pooled_free(occ, occ_bytes, device, vr_host::Readers(readers));
     vr_host::pooled_free(ptr, bytes, device, std::move(readers));
   }
 };
@@ -375,6 +381,30 @@ void build_zpair(DevBuf *b, hipStream_t s) {
   VR_HIP(hipStreamSynchronize(s));
 }
 
+// The occupancy map of buffer b (DevBuf::occ) for the march's empty-space probe, rebuilt with every
+// upload into it (its readers have completed); none for small volumes (the probe needs a map only
+// where leaps are long) or with VR_NO_PROBE=1.
+#ifndef VR_OCC_MIN_VOXELS
+#define VR_OCC_MIN_VOXELS (1ull << 18)
+#endif
+void build_occupancy(DevBuf *b, hipStream_t s) {
+  const uint64_t px = b->dims[0] + 2, py = b->dims[1] + 2, pz = b->dims[2] + 2;
+  const bool want = px * py * pz >= VR_OCC_MIN_VOXELS && px < (1ull << 31) && !env_flag("VR_NO_PROBE");
+  const uint64_t bytes = want ? ((px + 7) / 8) * ((py + 7) / 8) * ((pz + 7) / 8) : 0;
+  if (!want || b->occ_bytes != bytes) {
+    if (b->occ) vr_host::pooled_free(b->occ, b->occ_bytes, b->device, vr_host::Readers(b->readers));
+    b->occ = nullptr;
+    b->occ_bytes = 0;
+  }
+  if (!want) return;
+  if (!b->occ) {
+    VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->occ), bytes, b->device));
+    b->occ_bytes = bytes;
+  }
+  VR_HIP(vr::launch_occupancy(b->ptr, (uint32_t)px, (uint32_t)py, (uint32_t)pz, b->occ, s));
+  VR_HIP(hipStreamSynchronize(s));
+}
+
 void sync_volume(vr_context *h, int tex, int slot) {
   g_tex.bind[tex].reset();
   const VolRec &v = h->vol[slot];
@@ -402,6 +432,9 @@ void sync_volume(vr_context *h, int tex, int slot) {
     b->nonfinite = st.nonfinite != 0;
     b->maxabs = st.maxabs;
     if (tex == T_LIGHT) build_zpair(b.get(), U.stream);
+    else build_occupancy(b.get(), U.stream);
+  } else {
+    build_occupancy(b.get(), nullptr);  // (an empty volume: drops a previous map)
   }
   b->version = next_version();
   b->src_data = v.data;
@@ -676,6 +709,12 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
   P.focal = f;
   // textures through the slot indices (getTexture, kernel.cu:127-144)
   P.em = dev_tex(g_tex.bind[g_tex.idx_em]);
+  {  // the emission buffer's occupancy map (the empty-space probe; null: none, no probe)
+    const BufPtr &eb = g_tex.bind[g_tex.idx_em];
+    P.occ = (eb && eb->ptr && eb->occ) ? eb->occ : nullptr;
+    P.occ_bx = P.occ ? (uint32_t)((eb->dims[0] + 2 + 7) / 8) : 0u;
+    P.occ_bxy = P.occ ? P.occ_bx * (uint32_t)((eb->dims[1] + 2 + 7) / 8) : 0u;
+  }
   P.ab = dev_tex(g_tex.bind[g_tex.idx_ab]);
   P.re = dev_tex(g_tex.bind[g_tex.idx_re]);
   P.gem = dev_tex(g_tex.bind[T_EM]);
@@ -827,7 +866,12 @@ int validate_partition(const vr_partition *p) {
 // the staging halo's rounding margin covers that many sequential additions.
 int chunk_samples(int K) { return K >= 2 ? 16 * K : 32; }
 void set_chunk_halo(Frame &F, int K) {
-  for (int i = 0; i < 3; ++i) F.P.tap_off[i] += (float)(chunk_samples(K) * F.drift1[i]);
+  for (int i = 0; i < 3; ++i) {
+    F.P.tap_off[i] += (float)(chunk_samples(K) * F.drift1[i]);
+    // the empty-space probe's box: the centre taps (the cell of floor(c n - 1/2)) with the staging
+    // margin of 1/16 texel, plus the drift of up to VR_PROBE_MAX sequential additions
+    F.P.probe_off[i] = (float)(0.0625 + (double)VR_PROBE_MAX * F.drift1[i]);
+  }
 }
 
 void free_views(vr_context *h) {
@@ -1223,6 +1267,19 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
                                         vr::fast::march_blocks_k4,
                                         VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
       P.view_blocks = vfns[ki](P);
+      // VR_STEREO_PAIR=1 (measurement): paired tiles -- the left eye's rays of
+      // column c + shift share a wave (and its staged box) with the right eye's of column c, the
+      // shift (whole tiles) making the two bundles meet at the volume's centre, at distance `dist`
+      // from the eyes: base * W * f / dist columns
+      if (env_flag("VR_STEREO_PAIR") && K > 1 && P.fast_shade && F.mode == 1 && F.ab_alias && P.tap_half &&
+          !P.wide_slot && !F.big && P.num_parts == 1 && !P.wg_order) {
+        const double base = std::fabs((double)a->props[0]), f = std::fabs((double)a->props[1]),
+                     dist = std::fabs((double)a->props[2]);
+        const int TW = 4;  // tile width at K = 2, 4 (vr_march.hip TileShape)
+        const double cols = dist > 0 ? base * (double)P.width * f / dist : 0.0;
+        P.pair_shift = (int32_t)std::min<double>(std::floor(cols / TW + 0.5) * TW, (double)P.width);
+        if (const char *ev = std::getenv("VR_STEREO_PAIR_SHIFT")) P.pair_shift = std::max(0, std::atoi(ev));
+      }
     }
     // diagnostics (VR_SCHED_DUMP): a timed launch also records its blocks' start ticks
     const char *dump = (P.wg_cost && P.sched_full != 2) ? std::getenv("VR_SCHED_DUMP") : nullptr;
@@ -1309,6 +1366,7 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
   if (F.mode == 2 || !F.ab_alias) return fail(VR_ERR_UNSUPPORTED, "slab render: lookup gradients / separate absorption");
   // the resident planes addressed by their global padded index: virtual base z_first planes back
   const bool re_em = P.re_is_em != 0;
+  P.occ = nullptr;  // (the probe is not used by the slab march; the map would be the slab's own)
   P.em.p = P.em.p - (ptrdiff_t)(sl->z_first * (uint64_t)P.em.pxy);
   P.em.nz = (int32_t)sl->depth;
   P.em.fnz = (float)sl->depth;
@@ -1425,8 +1483,24 @@ BufPtr replicate(const BufPtr &b, int dev, hipStream_t s, bool peer = true) {
     vr_host::EventPtr ev;
     if (peer) {
       VR_HIP(hipMemcpyPeerAsync(r->ptr, dev, b->ptr, b->device, b->bytes, s));
+      // the occupancy map along with it (peer copies only; a staged replica marches without probes)
+      if (b->occ && r->occ_bytes != b->occ_bytes) {
+        if (r->occ) vr_host::pooled_free(r->occ, r->occ_bytes, dev, vr_host::Readers(r->readers));
+        r->occ = nullptr;
+        r->occ_bytes = 0;
+        DeviceGuard dg(dev);
+        VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&r->occ), b->occ_bytes, dev));
+        r->occ_bytes = b->occ_bytes;
+      }
+      if (b->occ) VR_HIP(hipMemcpyPeerAsync(r->occ, dev, b->occ, b->device, b->occ_bytes, s));
       VR_HIP(vr_host::record_event(s, ev));
-    } else {  // no peer mapping: through pinned host memory (b is resident: its D2H runs now)
+    }
+    if (!(peer && b->occ) && r->occ) {  // no map copied: none (a stale one would leap wrongly)
+      vr_host::pooled_free(r->occ, r->occ_bytes, dev, vr_host::Readers(r->readers));
+      r->occ = nullptr;
+      r->occ_bytes = 0;
+    }
+    if (!peer) {  // no peer mapping: through pinned host memory (b is resident: its D2H runs now)
       if (b->ready) vr_host::wait(b->ready);
       ev = staged_copy(r->ptr, dev, s, b->ptr, b->device, nullptr, b->bytes);
     }
@@ -2232,6 +2306,28 @@ int vr_render_stereo(vr_context *h, const vr_render_args *a, float base, float *
     VR_HIP(hipMemcpy(out_right, d_right, bytes, hipMemcpyDeviceToHost));
   }
   return VR_OK;
+  VR_GUARD_END
+}
+
+int vr_render_stereo_device(vr_context *h, const vr_render_args *a, float base, float *d_left, float *d_right,
+                            unsigned long long *d_steps, void *stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!valid(h)) return fail(VR_ERR_HANDLE, "Handle not valid.");
+  if (!a) return fail(VR_ERR_ARGUMENT, "insufficient parameter!");
+  if (!h->children.empty()) return fail(VR_ERR_UNSUPPORTED, "vr_render_stereo_device: one-device handles only");
+  VR_GUARD_BEGIN
+  DeviceGuard dg(h->device);
+  vr_host::prune_retired();
+  if ((size_t)a->resolution[0] * (size_t)a->resolution[1] && (!d_left || !d_right))
+    return fail(VR_ERR_ARGUMENT, "output is NULL");
+  vr_render_args al = *a;  // as vr_render_stereo: left = -base (the frame's eye), right = +base
+  al.props[0] = -base;
+  const float *r = a->rotation_flipped;
+  const float X[3] = {r[2], r[1], r[0]}, Z[3] = {r[8], r[7], r[6]};
+  float eye2[3];
+  for (int i = 0; i < 3; ++i) eye2[i] = fmaf(-a->props[2], Z[i], base * X[i]);
+  Frame F;
+  return do_render(h, &al, nullptr, d_left, d_steps, (hipStream_t)stream, F, d_right, eye2);
   VR_GUARD_END
 }
 

@@ -25,6 +25,12 @@ struct DevTex {
   const float *zp;  // small textures: the z-paired copy (vr_kernels.hip zpair_kernel), or null
 };
 
+// Longest run of samples the march's empty-space probe leaps at once (vr_stage.h probe_run); the
+// host's probe margin (RenderParams::probe_off) covers the position drift of that many additions.
+#ifndef VR_PROBE_MAX
+#define VR_PROBE_MAX 512
+#endif
+
 // One light in kernel order (position reversed from MATLAB, render.cpp:167-168).
 struct DevLight {
   float px, py, pz;
@@ -79,6 +85,8 @@ struct RenderParams {
   float *out;                     // [3][plane_cols][H]: column-major planar image of the part
   float *out2;                    // fused stereo: the second view's image
   int32_t views;                  // 1, or 2 = both stereo eyes in one launch (vr_render_stereo)
+  int32_t pair_shift;             // views 2: 0 (each workgroup one eye), or paired tiles -- a wave
+                                  // marches the right eye's columns c.. with the left eye's c + shift..
   uint32_t view_blocks;           // workgroups per view (the launch has views x view_blocks)
   // launch schedule: workgroup b marches tile block wg_order[b] (null: b); each
   // block's duration in s_memrealtime ticks is stored to wg_cost[block] (null: not recorded)
@@ -91,6 +99,13 @@ struct RenderParams {
                                   // 2 following the last measured order without timing
   uint32_t prio_blocks;           // scheduled launch: the first prio_blocks workgroups (the longest)
                                   // run at raised wave priority
+  // empty-space probe (round 5, vr_stage.h probe_run): the emission texture's occupancy map -- one
+  // byte per 8x8x8 brick of the padded volume, 0 when every voxel of the brick is +-0 -- or null;
+  // its row and plane pitch in bricks; per axis the probe's margin in texels (the centre taps'
+  // rounding margin plus the drift of VR_PROBE_MAX sequential position additions)
+  const uint8_t *occ;
+  uint32_t occ_bx, occ_bxy;
+  float probe_off[3];
   unsigned long long *steps;      // optional sample counter
   // sort-last slab launch (vr_render_slab): owned normalized z range [slab_z0,
   // slab_z1), the margin of the chunk ownership test, the resident padded planes [slab_pk0,

@@ -588,6 +588,40 @@ __global__ void zpair_kernel(const float *src, float *dst, uint32_t n, uint32_t 
   reinterpret_cast<float2 *>(dst)[i] = make_float2(a, b);
 }
 
+// Occupancy map of a padded (apron-layout) volume for the march's empty-space probe (vr_stage.h
+// probe_run): one byte per 8x8x8 brick, 1 when any voxel of the brick is non-zero (NaN included,
+// +-0 not: the test the staging copy applies to its box, vr_stage.h stage_box).  A workgroup takes a
+// 256-voxel run of x in one (y, z) brick row and ORs its 64 rows (coalesced 1 KiB row loads); eight
+// consecutive lanes then hold one brick.
+__global__ __launch_bounds__(256) void occupancy_kernel(const float *__restrict__ p, uint32_t px, uint32_t py,
+                                                        uint32_t pz, uint8_t *__restrict__ occ, uint32_t obx,
+                                                        uint32_t oby) {
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t by = blockIdx.y, bz = blockIdx.z;
+  uint32_t acc = 0;
+  if (x < px) {
+    const uint64_t pxy = (uint64_t)px * py;
+#pragma unroll 8
+    for (uint32_t k = 0; k < 64; ++k) {
+      const uint32_t y = by * 8u + (k & 7u), z = bz * 8u + (k >> 3);
+      if (y < py && z < pz) acc |= __float_as_uint(p[(uint64_t)z * pxy + (uint64_t)y * px + x]) & 0x7fffffffu;
+    }
+  }
+  acc |= (uint32_t)__shfl_xor((int)acc, 1, 64);
+  acc |= (uint32_t)__shfl_xor((int)acc, 2, 64);
+  acc |= (uint32_t)__shfl_xor((int)acc, 4, 64);
+  if ((threadIdx.x & 7u) == 0 && x < px) occ[((uint64_t)bz * oby + by) * obx + (x >> 3)] = acc != 0u ? 1 : 0;
+}
+
+hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, hipStream_t s) {
+  if (!px || !py || !pz) return hipSuccess;
+  const uint32_t obx = (px + 7) / 8, oby = (py + 7) / 8, obz = (pz + 7) / 8;
+  if (oby > 65535 || obz > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(occupancy_kernel, dim3((px + 255) / 256, oby, obz), dim3(256), 0, s, p, px, py, pz, occ, obx,
+                     oby);
+  return hipGetLastError();
+}
+
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(zpair_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, dst, n, pxy);

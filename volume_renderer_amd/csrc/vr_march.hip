@@ -156,8 +156,18 @@ __device__ __forceinline__ void first_of_group(float flagf, float t0, const f3 &
 }
 
 struct ChunkStats {
-  uint32_t staged, leap, fall, iter, lit;
+  uint32_t staged, leap, fall, iter, lit, probe, probe_fail;
 };
+
+#ifndef VR_PROBE
+#define VR_PROBE 1  // the empty-space probe (vr_stage.h probe_run); 0: staged empty-chunk leaps only
+#endif
+#ifndef VR_PROBE_RETRY
+#define VR_PROBE_RETRY 1
+#endif
+#ifndef VR_PROBE_MIN
+#define VR_PROBE_MIN (2 * VR_CHUNK)  // the probe's first run after the march enters empty space
+#endif
 
 // One sample of a ray at position `pos` (volumeRender_kernel.cu:444-474): the emission /
 // absorption fetch, opacity, and for a lit, non-empty sample the gradient and the shading.  Returns
@@ -435,7 +445,7 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // state becomes the resume point (store_resume).
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
-                                      uint32_t kk = 0) {
+                                      uint32_t kk = 0, KParams kp = nullptr) {
   static_assert(!COUNT || K == 1 || VR_COUNT_K, "the counter variant is built for K = 1 only (VR_COUNT_K: all K)");
   static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
   const int cap = P.max_steps;
@@ -456,6 +466,13 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   // instead of always VR_CHUNK halved until it fits: fewer box reductions per chunk.  The samples
   // are the same whatever the chunk length (the staging never changes a result).
   int s0 = VR_CHUNK;
+  // Empty-space probe (vr_stage.h probe_run; tame waves, absorption = emission, not the slab march):
+  // ps > 0 -- the next probe's run length (doubled after each empty run, up to VR_PROBE_MAX); 0 --
+  // off (a probe found data: the staged chunks go on until they find data themselves); -1 -- armed
+  // (a chunk found data; the next empty chunk restarts the probe at VR_PROBE_MIN).  Rays start in
+  // front of the data, so the probe starts on.
+  constexpr bool PROBE = VR_PROBE && !NANCHK && AB_ALIAS && !SLAB;
+  int ps = VR_PROBE_MIN;
   // the tame reflection's single voxel (sample_at), held in a register across the march: an opaque
   // copy, so that the compiler does not re-issue the invariant load in every sample
   float rv = 0.f;
@@ -477,7 +494,38 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     }
     if (two) pre = pre2;
   }
+  // the recurrences of n samples whose every sample adds exactly nothing (an empty-chunk leap or an
+  // empty probe run); tame waves: one exit test after the n additions (advance_n; t only grows)
+  auto leap_run = [&](int n) __attribute__((always_inline)) {
+    if constexpr (K == 1) {
+      if (COUNT || !VR_BRANCHFREE_LEAP) leap(P, n, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // exact counts
+      else if constexpr (!NANCHK) advance_n(P, n, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+      else advance(P, n, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+    } else {
+      if constexpr (!NANCHK) advance_n(P, n, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+      else advance(P, n, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+      R.alive = R.alive && group_any<K>(R.mine);
+    }
+  };
   while (__any(R.alive)) {
+    if constexpr (PROBE) {
+      if (ps > 0 && kp != nullptr && kparams_fresh(kp)->occ != nullptr) {
+        const bool live = K > 1 ? (R.alive && R.mine) : R.alive;
+        int e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
+        if (VR_PROBE_RETRY && e < 0 && ps > VR_PROBE_MIN) {  // too many bricks: a run half as long
+          ps >>= 1;
+          e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
+        }
+        if (e > 0) {
+          if (COUNT) ++C.probe;
+          leap_run(ps);
+          ps = min(2 * ps, (int)VR_PROBE_MAX);
+          continue;
+        }
+        if (COUNT) ++C.probe_fail;
+        ps = 0;
+      }
+    }
     // ---- chunk set-up: the box of every tap the live rays take in the next S samples --------
     int S;
     bool staged, partial;
@@ -533,18 +581,11 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     const bool whole = __builtin_amdgcn_readfirstlane((!NANCHK && !SLAB && staged && !partial && !edge) ? 1 : 0) != 0;
 
     if (empty) {
-      // tame waves: one exit test after the S additions (advance_n; t only grows)
-      if constexpr (K == 1) {
-        if (COUNT || !VR_BRANCHFREE_LEAP) leap(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);  // exact counts
-        else if constexpr (!NANCHK) advance_n(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
-        else advance(P, S, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
-      } else {
-        if constexpr (!NANCHK) advance_n(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
-        else advance(P, S, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
-        R.alive = R.alive && group_any<K>(R.mine);
-      }
+      leap_run(S);
+      if (PROBE && ps < 0) ps = VR_PROBE_MIN;  // back in empty space after data: probe again
       continue;
     }
+    if (PROBE) ps = -1;  // data: armed
 
     // ---- S samples ---------------------------------------------------------------------------
     if constexpr (K == 1) {
@@ -697,32 +738,54 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n, int run) {
 // (the occupancy cap of the unscheduled kernel); 3: a full frame following the order without
 // recording durations.  (Round 4: two chord-split schedules, SCHED 4 / 5, measured slower and
 // removed in round 5 -- DESIGN.md s8, s9.)
+// SCHED 4 (round 5, fused stereo with paired tiles, P.pair_shift > 0; DESIGN.md s9 "shared reads"):
+// each wave marches half a tile of each eye -- the right eye's rays of columns c .. c + TW - 1 and
+// the left eye's of columns c + pair_shift .., the shift chosen so that the two bundles converge at
+// the volume's centre -- so that one staged box (the union of the two bundles' footprints) serves
+// both eyes.  Columns are counted on a virtual image of part_cols + pair_shift columns: the left
+// eye's pixel at virtual column xv, the right eye's at xv - pair_shift; every pixel of each eye
+// is marched once.  Unpartitioned frames only.
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float *L = lds[wave];
+  constexpr bool ORDERED = SCHED >= 1 && SCHED <= 3;
   constexpr bool TIMED = SCHED == 1 || SCHED == 2;  // SCHED 3: the order only
+  constexpr bool PAIRED = SCHED == 4;
   const uint64_t clk0 = TIMED ? __builtin_amdgcn_s_memrealtime() : 0;
-  uint32_t wgo = SCHED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
-  if (!SCHED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
+  uint32_t wgo = ORDERED ? P.wg_order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x, P.xcd_run);
+  if (!ORDERED && P.block_rot) {  // (A/B, VR_BLOCK_ROT_ROWS) a rotation of the row-major order
     wgo += P.block_rot;
     if (wgo >= gridDim.x) wgo -= gridDim.x;
   }
   // the longest blocks (first in the order) issue ahead of the short ones that fill in beside them
-  if (SCHED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
-  // fused stereo: the second view's workgroups follow the first's (same rays, other eye)
-  const int view = (P.views > 1 && wgo >= P.view_blocks) ? 1 : 0;
-  const uint32_t wg = view ? wgo - P.view_blocks : wgo;
+  if (ORDERED && blockIdx.x < P.prio_blocks) __builtin_amdgcn_s_setprio(2);
+  int view, lc, y;
+  if constexpr (PAIRED) {
+    constexpr int TH2 = TS::TH / 2, HR = (64 / K) / 2;  // rows and rays of each eye's half tile
+    const int tile = (int)wgo * VR_WG_WAVES + wave;
+    const int nbx = (P.part_cols + P.pair_shift + 2 * TS::TW - 1) / (2 * TS::TW);
+    const int blk = tile >> 2, quad = tile & 3;
+    const int ray = lane >> TS::LK, rr = ray & (HR - 1);
+    view = ray >= HR ? 0 : 1;  // 0: the left eye (P.out), 1: the right eye (P.out2)
+    const int xv = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + rr / TH2;
+    y = (blk / nbx) * (2 * TH2) + (quad >> 1) * TH2 + rr % TH2;
+    lc = view ? xv - P.pair_shift : xv;
+  } else {
+    // fused stereo: the second view's workgroups follow the first's (same rays, other eye)
+    view = (P.views > 1 && wgo >= P.view_blocks) ? 1 : 0;
+    const uint32_t wg = view ? wgo - P.view_blocks : wgo;
+    const int tile = (int)wg * VR_WG_WAVES + wave;
+    const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
+    const int blk = tile >> 2, quad = tile & 3;
+    const int ray = lane >> TS::LK;
+    lc = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + (ray / TS::TH);
+    y = (blk / nbx) * (2 * TS::TH) + (quad >> 1) * TS::TH + (ray % TS::TH);
+  }
   float *const out = view ? P.out2 : P.out;
-  const int tile = (int)wg * VR_WG_WAVES + wave;
-  const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
-  const int blk = tile >> 2, quad = tile & 3;
-  const int ray = lane >> TS::LK;
-  const int lc = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + (ray / TS::TH);
-  const int y = (blk / nbx) * (2 * TS::TH) + (quad >> 1) * TS::TH + (ray % TS::TH);
-  const bool active = (lc < P.part_cols) && (y < P.height);
+  const bool active = (!PAIRED || lc >= 0) && (lc < P.part_cols) && (y < P.height);
   Ray R;
   R.o = mk(0.f, 0.f, 0.f);
   R.pos = R.o;
@@ -732,7 +795,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   R.sr = R.sg = R.sb = R.sa = 0.f;
   R.nsteps = R.nlit = 0;
   R.alive = false;
-  ChunkStats C{0, 0, 0, 0, 0};
+  ChunkStats C{0, 0, 0, 0, 0, 0, 0};
   if (active) {
     const int blk = lc / P.block_cols, within = lc - blk * P.block_cols;
     const int x = (P.part + blk * P.num_parts) * P.block_cols + within;
@@ -746,7 +809,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   // every coordinate the march forms from a finite start and step is finite; a tame launch takes
   // the fast path (sample_at: TAME)
   if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C, 0u, (KParams)__builtin_amdgcn_kernarg_segment_ptr());
   else
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
@@ -781,6 +844,8 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
       atomicAdd(P.steps + 4, (unsigned long long)C.fall);
       atomicAdd(P.steps + 5, (unsigned long long)C.iter);
       atomicAdd(P.steps + 6, (unsigned long long)C.lit);
+      atomicAdd(P.steps + 7, (unsigned long long)C.probe);
+      atomicAdd(P.steps + 44, (unsigned long long)C.probe_fail);
     }
   }
 }
@@ -791,7 +856,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
 // through this function its register allocation changes, and the metric kernel is measured as is.)
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP>
 __device__ __forceinline__ void march_tile(const RenderParams &P, float *L, int lane, int wave, uint32_t wg,
-                                           int view, float *out, Ray &R, ChunkStats &C) {
+                                           int view, float *out, Ray &R, ChunkStats &C, KParams kp) {
   using TS = TileShape<K>;
   const int tile = (int)wg * VR_WG_WAVES + wave;
   const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
@@ -821,7 +886,7 @@ __device__ __forceinline__ void march_tile(const RenderParams &P, float *L, int 
   // every coordinate the march forms from a finite start and step is finite; a tame launch takes
   // the fast path (sample_at: TAME)
   if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C);
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C, 0u, kp);
   else
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
@@ -847,9 +912,12 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, false)) void ma
   const uint32_t view = blockIdx.x / per_view;
   const RenderParams &P = V.p[view];
   Ray R;
-  ChunkStats C{0, 0, 0, 0, 0};
+  ChunkStats C{0, 0, 0, 0, 0, 0, 0};
+  // (view's RenderParams in the argument segment: V is the kernel's first argument)
+  const KParams kp = (KParams)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() +
+                               (size_t)view * sizeof(RenderParams));
   march_tile<K, MODE, AB_ALIAS, false, false, false, CAP>(P, lds[wave], lane, wave, blockIdx.x - view * per_view, 0,
-                                                          P.out, R, C);
+                                                          P.out, R, C, kp);
 }
 
 #if !VR_ISA_PROBE
@@ -937,7 +1005,7 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, (CAP <= VR_LDS_CAP && !SCHED) ? V
   R.mine = false;
   R.past = false;
   bool go_on = true;  // the incoming state: the ray has not terminated
-  ChunkStats C{0, 0, 0, 0, 0};
+  ChunkStats C{0, 0, 0, 0, 0, 0, 0};
   if (active) {
     f3 d;
     float tnear;
@@ -1042,6 +1110,19 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
     hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, 0, s, P);          \
     note_march_kernel(VR_MARCH_FAST, KK, MODE, AB, CNT, SH, BG, CAP, SC);                                 \
   } while (0)
+  // paired stereo tiles (SCHED 4): the lit, half-texel-tap, absorption = emission, default-slot,
+  // 32-bit launch of K > 1 only (a measurement of what the eyes' staged boxes share)
+  constexpr bool PAIRK = K > 1 && VR_MARCH_FAST && AB && MODE == 1 && SH && CAP == VR_LDS_CAP;
+  if (P.pair_shift) {
+    if constexpr (PAIRK) {
+      if (big || sched || (P.steps && !VR_COUNT_K)) return hipErrorInvalidValue;
+      if (P.steps) VR_LAUNCH(K, VR_COUNT_K != 0, false, 4);
+      else VR_LAUNCH(K, false, false, 4);
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
   // (the counter variant: instantiated in the K = 1 object only -- or at every K in a VR_COUNT_K build)
   if constexpr (K == 1 || VR_COUNT_K) {
     if (P.steps) {
@@ -1099,7 +1180,13 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
                          (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
   const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
   if (P.views > 1 && (P.view_blocks != per_view || !P.out2)) return hipErrorInvalidValue;
-  const dim3 grid(per_view * (P.views > 1 ? 2u : 1u));
+  dim3 grid(per_view * (P.views > 1 ? 2u : 1u));
+  if (P.pair_shift) {  // paired stereo tiles (march_kernel SCHED 4): half tiles of each eye over the virtual width
+    if (P.views != 2 || P.num_parts != 1 || P.pair_shift < 0 || P.wg_order) return hipErrorInvalidValue;
+    const uint64_t ptiles = (uint64_t)((P.part_cols + P.pair_shift + 2 * TS::TW - 1) / (2 * TS::TW)) *
+                            (uint64_t)((P.height + TS::TH - 1) / TS::TH) * 4;
+    grid = dim3((unsigned)((ptiles + VR_WG_WAVES - 1) / VR_WG_WAVES));
+  }
   if (P.wg_order && (P.sched_blocks != grid.x || !P.wg_cost || VR_MARCH_K == 1))
     return hipErrorInvalidValue;  // a schedule of another grid, or for K = 1 (not built)
   switch (mode) {

@@ -425,6 +425,77 @@ __device__ __forceinline__ void plan_chunk(const RenderParams &P, bool alive, co
   S >>= 1;  // no box fits: march S/2 samples from global memory
 }
 
+// The launch's RenderParams in the kernel-argument segment (march_kernel: the first argument, at
+// offset 0; march_views_kernel: view v's entry), for parameters read at their point of use with
+// scalar loads the compiler cannot hoist (the empty-space probe's: read once per probe, not held in
+// SGPRs across the sample loop).  Formed from __builtin_amdgcn_kernarg_segment_ptr, never from the
+// address of the by-value parameter (which may be a private copy).
+typedef const __attribute__((address_space(4))) RenderParams *KParams;
+__device__ __forceinline__ KParams kparams_fresh(KParams kp) {
+  asm volatile("" : "+s"(kp));
+  return kp;
+}
+
+// Empty-space probe (round 5): whether every centre tap of the live rays' next L
+// samples lies in bricks of the emission texture's occupancy map (RenderParams::occ) that hold only
+// +-0 -- then each of those samples has em = ab = 0 and opacity exactly 0, adds exactly nothing
+// (skip_empty), and the rays may leap the L samples replaying only the recurrences, as the
+// empty-chunk leap does after staging an all-zero box.  Here no box is staged: one byte per brick
+// of the box's bricks is read (one load per lane, two for up to 128 bricks), so a run through
+// empty space costs a box reduction and one round trip per L samples instead of a staging copy per
+// chunk.  The box is the centre cells' range with RenderParams::probe_off as the margin (the
+// gradient taps do not matter: an opacity-0 sample is never shaded).  Returns 1: empty (leap),
+// 0: a brick is occupied, -1: the box spans more than 128 bricks (undecided).  Wave-uniform.
+__device__ __forceinline__ int probe_run(const RenderParams &P, KParams kp0, bool alive, const f3 &pos,
+                                         const f3 &step, float t, float tfar, int L, int lane) {
+  const KParams kp = kparams_fresh(kp0);
+  const DevTex &E = P.em;
+  const f3 bmin = mk(P.bmin[0], P.bmin[1], P.bmin[2]);
+  const f3 bsc = mk(P.bscale[0], P.bscale[1], P.bscale[2]);
+  int lo[3] = {0x3fffffff, 0x3fffffff, 0x3fffffff}, hi[3] = {-0x3fffffff, -0x3fffffff, -0x3fffffff};
+  bool edge = false;
+  if (alive) {
+    const float rem = (tfar - t) / P.tstep;  // samples left before the exit test fires
+    const int s_eff = (rem < (float)L) ? max((int)rem + 2, 1) : L;
+    const float k = (float)(s_eff - 1);
+    const f3 pe = mk(fmaf(step.x, k, pos.x), fmaf(step.y, k, pos.y), fmaf(step.z, k, pos.z));
+    axis_range(((pos.x - bmin.x) * bsc.x) * E.fnx - 0.5f, ((pe.x - bmin.x) * bsc.x) * E.fnx - 0.5f,
+               kp->probe_off[0], E.nx, lo[0], hi[0], edge);
+    axis_range(((pos.y - bmin.y) * bsc.y) * E.fny - 0.5f, ((pe.y - bmin.y) * bsc.y) * E.fny - 0.5f,
+               kp->probe_off[1], E.ny, lo[1], hi[1], edge);
+    axis_range(((pos.z - bmin.z) * bsc.z) * E.fnz - 0.5f, ((pe.z - bmin.z) * bsc.z) * E.fnz - 0.5f,
+               kp->probe_off[2], E.nz, lo[2], hi[2], edge);
+  }
+  // brick ranges of the box (padded coordinates / 8): lo in the low, -hi in the high int16 field
+  const int c = 16383;
+  const int a = wave_min2(pk2(min(lo[0] >> 3, c), min(lo[1] >> 3, c)));
+  const int b = wave_min2(pk2(min(lo[2] >> 3, c), min(-(hi[0] >> 3), c)));
+  const int d = wave_min2(pk2(min(-(hi[1] >> 3), c), min(-(hi[2] >> 3), c)));
+  const int bx = pk_lo(a), by = pk_hi(a), bz = pk_lo(b);
+  const int cx = -pk_hi(b) - bx + 1, cy = -pk_lo(d) - by + 1, cz = -pk_hi(d) - bz + 1;
+  if (cx <= 0 || cy <= 0 || cz <= 0) return 1;  // no live ray
+  const int cnt = cx * cy * cz;
+  if (cnt > 128) return -1;
+  // lane q -> brick q and q + 64 of the box (x fastest); the divisions by the uniform extents in fp32
+  // (q < 128 and extents <= 128: exact quotients after the truncation)
+  const float rcx = 1.f / (float)cx, rcy = 1.f / (float)cy;
+  const uint8_t *occ = kp->occ;
+  const uint32_t obx = kp->occ_bx, obxy = kp->occ_bxy;
+  uint32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = lane + 64 * j;
+    if (q < cnt) {
+      const int qz = (int)(((float)q + 0.5f) * (rcx * rcy));
+      const int r = q - qz * cx * cy;
+      const int qy = (int)(((float)r + 0.5f) * rcx);
+      const int qx = r - qy * cx;
+      v |= occ[(uint32_t)(bz + qz) * obxy + (uint32_t)(by + qy) * obx + (uint32_t)(bx + qx)];
+    }
+  }
+  return __any(v != 0u) ? 0 : 1;
+}
+
 // The empty-chunk leap: every tap of the chunk lies in the staged all-zero box, so each sample has
 // em = ab = 0, alpha = 1 - exp(-0) = 0 and adds exactly 0 (skip_empty proves the shading term
 // finite).  Only the march recurrences run, in the reference's order.

@@ -222,6 +222,16 @@ def render_device(handle, ra: VrRenderArgs, d_out: int, part=None, d_steps: int 
                                  ctypes.c_void_p(int(stream)) if stream else None))
 
 
+def render_stereo_device(handle, ra: VrRenderArgs, base: float, d_left: int, d_right: int, d_steps: int = 0,
+                         stream: int = 0) -> None:
+    """Both eyes of a stereo pair into device memory in one launch (vr_render_stereo_device): the
+    left eye (camera offset -base) to d_left, the right (+base) to d_right; ra.props[0] is ignored."""
+    check(lib().vr_render_stereo_device(_handle(handle), ctypes.byref(ra), ctypes.c_float(base),
+                                        ctypes.c_void_p(int(d_left)), ctypes.c_void_p(int(d_right)),
+                                        ctypes.c_void_p(int(d_steps)) if d_steps else None,
+                                        ctypes.c_void_p(int(stream)) if stream else None))
+
+
 def last_march_kernel() -> str:
     """The demangled name of the march kernel instantiation the last render launched."""
     buf = ctypes.create_string_buffer(256)
