@@ -184,10 +184,11 @@ int vr_sum_channels_device(const float *d_in, int32_t n, int32_t views, uint64_t
  * If d_steps != NULL it points to VR_NUM_COUNTERS (48) counters: d_steps[0] += ray-march samples
  * taken, d_steps[1] += samples that evaluated gradient + shading (the others had opacity exactly
  * 0), d_steps[2..4] += LDS-staged chunks, all-empty (leaped) chunks, global-memory chunks,
- * d_steps[5..6] += wave sample iterations, of which any lane shaded; d_steps[7] reserved;
- * d_steps[8..39] histogram of the box volume (floats, bins of 256, last bin open) of chunks that
- * fell back to global memory; d_steps[40..43] staged chunks with S = 32, 16, 8, 4.
- * [2..43] are filled by the LDS-staged kernel only. */
+ * d_steps[5..6] += wave sample iterations, of which any lane shaded; d_steps[7] += empty-space
+ * probe runs leaped; d_steps[8..39] histogram of the box volume (floats, bins of
+ * 256, last bin open) of chunks that fell back to global memory; d_steps[40..43] staged chunks with
+ * S = 32, 16, 8, 4; d_steps[44] += probes that found data; d_steps[45] += floats staged into LDS.
+ * [2..45] are filled by the LDS-staged kernel only. */
 #define VR_NUM_COUNTERS 48
 int vr_render_device(vr_context *h, const vr_render_args *args, const vr_partition *part,
                      float *d_out, unsigned long long *d_steps, void *stream);

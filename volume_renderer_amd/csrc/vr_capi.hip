@@ -390,7 +390,8 @@ void build_zpair(DevBuf *b, hipStream_t s) {
 void build_occupancy(DevBuf *b, hipStream_t s) {
   const uint64_t px = b->dims[0] + 2, py = b->dims[1] + 2, pz = b->dims[2] + 2;
   const bool want = px * py * pz >= VR_OCC_MIN_VOXELS && px < (1ull << 31) && !env_flag("VR_NO_PROBE");
-  const uint64_t bytes = want ? ((px + 7) / 8) * ((py + 7) / 8) * ((pz + 7) / 8) : 0;
+  constexpr uint64_t E = 1u << VR_OCC_LOG;  // brick edge
+  const uint64_t bytes = want ? ((px + E - 1) / E) * ((py + E - 1) / E) * ((pz + E - 1) / E) : 0;
   if (!want || b->occ_bytes != bytes) {
     if (b->occ) vr_host::pooled_free(b->occ, b->occ_bytes, b->device, vr_host::Readers(b->readers));
     b->occ = nullptr;
@@ -712,8 +713,9 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
   {  // the emission buffer's occupancy map (the empty-space probe; null: none, no probe)
     const BufPtr &eb = g_tex.bind[g_tex.idx_em];
     P.occ = (eb && eb->ptr && eb->occ) ? eb->occ : nullptr;
-    P.occ_bx = P.occ ? (uint32_t)((eb->dims[0] + 2 + 7) / 8) : 0u;
-    P.occ_bxy = P.occ ? P.occ_bx * (uint32_t)((eb->dims[1] + 2 + 7) / 8) : 0u;
+    constexpr uint64_t E = 1u << VR_OCC_LOG;
+    P.occ_bx = P.occ ? (uint32_t)((eb->dims[0] + 2 + E - 1) / E) : 0u;
+    P.occ_bxy = P.occ ? P.occ_bx * (uint32_t)((eb->dims[1] + 2 + E - 1) / E) : 0u;
   }
   P.ab = dev_tex(g_tex.bind[g_tex.idx_ab]);
   P.re = dev_tex(g_tex.bind[g_tex.idx_re]);
@@ -744,6 +746,10 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
       P.tap_off[i] = (float)((F.mode == 1 ? (double)P.gstep[i] * P.bscale[i] * n : 0.0) + 0.0625);
     }
     P.tap_half = half_texel_taps(P, F.mode, P.em.fnz);
+    // (n / 2 per axis, exact: n a power of two)
+    P.cube_hs[0] = P.tap_half ? P.em.fnx * 0.5f : 0.f;
+    P.cube_hs[1] = P.tap_half ? P.em.fny * 0.5f : 0.f;
+    P.cube_hs[2] = P.tap_half ? P.em.fnz * 0.5f : 0.f;
   }
   // Empty-sample skip: a sample with alpha == 0 adds fma(eds, c, ill) * 0 to the
   // sum; that is exactly +-0 (a no-op) whenever the illumination term `ill` is finite, which holds
@@ -1387,6 +1393,8 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
     F.drift1[2] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[2] * D;
     P.tap_off[2] = (float)((F.mode == 1 ? (double)P.gstep[2] * P.bscale[2] * D : 0.0) + 0.0625);
     P.tap_half = half_texel_taps(P, F.mode, (float)D);  // judged on the whole volume, as one render
+    for (int i = 0; i < 3; ++i)  // (the cube's n / 2 per axis, the whole volume's depth on z)
+      P.cube_hs[i] = P.tap_half ? (i == 0 ? P.em.fnx : i == 1 ? P.em.fny : (float)D) * 0.5f : 0.f;
   }
   P.slab_dir = sl->direction;
   P.slab_in = d_in;

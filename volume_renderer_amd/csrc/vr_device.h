@@ -31,6 +31,11 @@ struct DevTex {
 #define VR_PROBE_MAX 512
 #endif
 
+// log2 of the occupancy map's brick edge (voxels of the padded volume per brick and axis)
+#ifndef VR_OCC_LOG
+#define VR_OCC_LOG 3
+#endif
+
 // One light in kernel order (position reversed from MATLAB, render.cpp:167-168).
 struct DevLight {
   float px, py, pz;
@@ -60,6 +65,7 @@ struct RenderParams {
   float tap_off[3];               // gradient tap offset in emission texels (staging halo)
   int32_t tap_half;               // MODE 1: the tap offset is half a texel on every axis (fast
                                   // variant derives the taps from the centre, vr_sampling.h)
+  float cube_hs[3];               // tap_half: n / 2 per axis of the power-of-two box [-1, 1]^3 (axis_cube_s)
   int32_t num_lights;
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;

@@ -596,26 +596,27 @@ __global__ void zpair_kernel(const float *src, float *dst, uint32_t n, uint32_t 
 __global__ __launch_bounds__(256) void occupancy_kernel(const float *__restrict__ p, uint32_t px, uint32_t py,
                                                         uint32_t pz, uint8_t *__restrict__ occ, uint32_t obx,
                                                         uint32_t oby) {
+  constexpr uint32_t E = 1u << VR_OCC_LOG;  // brick edge
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   const uint32_t by = blockIdx.y, bz = blockIdx.z;
   uint32_t acc = 0;
   if (x < px) {
     const uint64_t pxy = (uint64_t)px * py;
 #pragma unroll 8
-    for (uint32_t k = 0; k < 64; ++k) {
-      const uint32_t y = by * 8u + (k & 7u), z = bz * 8u + (k >> 3);
+    for (uint32_t k = 0; k < E * E; ++k) {
+      const uint32_t y = by * E + (k & (E - 1)), z = bz * E + (k >> VR_OCC_LOG);
       if (y < py && z < pz) acc |= __float_as_uint(p[(uint64_t)z * pxy + (uint64_t)y * px + x]) & 0x7fffffffu;
     }
   }
-  acc |= (uint32_t)__shfl_xor((int)acc, 1, 64);
-  acc |= (uint32_t)__shfl_xor((int)acc, 2, 64);
-  acc |= (uint32_t)__shfl_xor((int)acc, 4, 64);
-  if ((threadIdx.x & 7u) == 0 && x < px) occ[((uint64_t)bz * oby + by) * obx + (x >> 3)] = acc != 0u ? 1 : 0;
+#pragma unroll
+  for (uint32_t m = 1; m < E; m <<= 1) acc |= (uint32_t)__shfl_xor((int)acc, (int)m, 64);
+  if ((threadIdx.x & (E - 1)) == 0 && x < px) occ[((uint64_t)bz * oby + by) * obx + (x >> VR_OCC_LOG)] = acc != 0u ? 1 : 0;
 }
 
 hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, hipStream_t s) {
   if (!px || !py || !pz) return hipSuccess;
-  const uint32_t obx = (px + 7) / 8, oby = (py + 7) / 8, obz = (pz + 7) / 8;
+  constexpr uint32_t E = 1u << VR_OCC_LOG;
+  const uint32_t obx = (px + E - 1) / E, oby = (py + E - 1) / E, obz = (pz + E - 1) / E;
   if (oby > 65535 || obz > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(occupancy_kernel, dim3((px + 255) / 256, oby, obz), dim3(256), 0, s, p, px, py, pz, occ, obx,
                      oby);

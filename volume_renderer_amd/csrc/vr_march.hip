@@ -159,11 +159,20 @@ struct ChunkStats {
   uint32_t staged, leap, fall, iter, lit, probe, probe_fail;
 };
 
+#ifndef VR_CUBE_AXIS
+#define VR_CUBE_AXIS 1  // the half-texel tap launch forms its axes as axis_cube_s (2 VALU instead of 4 per axis)
+#endif
 #ifndef VR_PROBE
 #define VR_PROBE 1  // the empty-space probe (vr_stage.h probe_run); 0: staged empty-chunk leaps only
 #endif
 #ifndef VR_PROBE_RETRY
 #define VR_PROBE_RETRY 1
+#endif
+#ifndef VR_PROBE_BISECT
+// 1: a probe that finds data (or too many bricks) retries at half the run length, down to
+// VR_PROBE_MIN -- the run stops closer to the data (same box: metric 28.4-28.6 -> 27.5 ms, C2 14.6 ->
+// 12.8 ms, P = 8 part 5.27 -> 5.07 ms, r5e)
+#define VR_PROBE_BISECT 1
 #endif
 #ifndef VR_PROBE_MIN
 #define VR_PROBE_MIN (2 * VR_CHUNK)  // the probe's first run after the march enters empty space
@@ -189,7 +198,16 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
   constexpr bool HALF_ONLY = HALF_TAPS && SHARE2;
   AxS sx{}, sy{}, sz{};
   Ax ax, ay, az;
-  if constexpr (HALF_TAPS) {
+  if constexpr (HALF_ONLY && VR_CUBE_AXIS) {
+    // the half-texel tap launch is a power-of-two cube (vr_capi.hip half_texel_taps): the
+    // coordinate in one add and one fma, bit-identical (vr_sampling.h axis_cube_s)
+    sx = axis_cube_s<NANCHK>(pos.x, P.cube_hs[0]);
+    sy = axis_cube_s<NANCHK>(pos.y, P.cube_hs[1]);
+    sz = axis_cube_s<NANCHK>(pos.z, P.cube_hs[2]);
+    ax = Ax{sx.i, sx.w};
+    ay = Ax{sy.i, sy.w};
+    az = Ax{sz.i, sz.w};
+  } else if constexpr (HALF_TAPS) {
     sx = axis_raw_s<NANCHK>(ps.x, E.fnx);
     sy = axis_raw_s<NANCHK>(ps.y, E.fny);
     sz = axis_raw_s<NANCHK>(ps.z, E.fnz);
@@ -512,7 +530,13 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       if (ps > 0 && kp != nullptr && kparams_fresh(kp)->occ != nullptr) {
         const bool live = K > 1 ? (R.alive && R.mine) : R.alive;
         int e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
-        if (VR_PROBE_RETRY && e < 0 && ps > VR_PROBE_MIN) {  // too many bricks: a run half as long
+        if (VR_PROBE_BISECT) {
+          // an occupied (or too large) box: runs half as long until one is empty or the shortest fails
+          while (e <= 0 && ps > VR_PROBE_MIN) {
+            ps >>= 1;
+            e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
+          }
+        } else if (VR_PROBE_RETRY && e < 0 && ps > VR_PROBE_MIN) {  // too many bricks: a run half as long
           ps >>= 1;
           e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
         }
@@ -565,6 +589,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     if (COUNT && lane == 0) {  // diagnostics: box volume of partial/failed chunks, S of staged ones
       if (!staged || partial) atomicAdd(P.steps + 8 + min(box_vol >> 8, 31), 1ull);
       else atomicAdd(P.steps + 40 + (S >= 32 ? 0 : (S >= 16 ? 1 : (S >= 8 ? 2 : 3))), 1ull);
+      if (staged) atomicAdd(P.steps + 45, (unsigned long long)(B.pxy * B.ez));  // staging volume (floats)
     }
     bool empty = false;
     if (staged) {

@@ -77,6 +77,22 @@ __device__ __forceinline__ AxS axis_raw_s(float c, float fn) {
   const float w = rintf(r * 256.f) * (1.f / 256.f);
   return AxS{(int)fl, w, r >= 0.5f};
 }
+// axis_raw_s of a power-of-two cube (box [-1, 1]: bmin = -1, bscale = 1/2; n = 2 hs a power of
+// two -- the half-texel tap launch, vr_capi.hip half_texel_taps): the sampler's coordinate
+// ((p - bmin) * bscale) * n - 1/2 is fma(p + 1, hs, -1/2) bit for bit -- p - (-1) is p + 1, and
+// the products by 1/2 and n (hs) are exact power-of-two scalings, so the fma's single rounding is
+// that of the final subtraction.  A NaN coordinate (p + 1 NaN) is taken as c = 0, i.e. p + 1 = 0.
+template <bool NANCHK = true>
+__device__ __forceinline__ AxS axis_cube_s(float p, float hs) {
+  float a = p + 1.f;
+  if (NANCHK) a = (a != a) ? 0.f : a;
+  const float xb = fmaf(a, hs, -0.5f);
+  const float fl = floorf(xb);
+  const float r = xb - fl;
+  const float w = rintf(r * 256.f) * (1.f / 256.f);
+  return AxS{(int)fl, w, r >= 0.5f};
+}
+
 // The two taps xb +- 1/2 of an axis derived from the centre's (fast shading variant, DESIGN.md
 // s4): with xb' = xb + 1/2 computed exactly, floor(xb') = i + hi and the quantized weight of
 // frac(xb') is w + 1/2 - hi (rint((r + 1/2 - hi) * 256) = rint(r * 256) + 128 - 256 hi: adding an

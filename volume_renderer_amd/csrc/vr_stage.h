@@ -466,11 +466,11 @@ __device__ __forceinline__ int probe_run(const RenderParams &P, KParams kp0, boo
     axis_range(((pos.z - bmin.z) * bsc.z) * E.fnz - 0.5f, ((pe.z - bmin.z) * bsc.z) * E.fnz - 0.5f,
                kp->probe_off[2], E.nz, lo[2], hi[2], edge);
   }
-  // brick ranges of the box (padded coordinates / 8): lo in the low, -hi in the high int16 field
+  // brick ranges of the box (padded coordinates >> VR_OCC_LOG): lo in the low, -hi in the high int16 field
   const int c = 16383;
-  const int a = wave_min2(pk2(min(lo[0] >> 3, c), min(lo[1] >> 3, c)));
-  const int b = wave_min2(pk2(min(lo[2] >> 3, c), min(-(hi[0] >> 3), c)));
-  const int d = wave_min2(pk2(min(-(hi[1] >> 3), c), min(-(hi[2] >> 3), c)));
+  const int a = wave_min2(pk2(min(lo[0] >> VR_OCC_LOG, c), min(lo[1] >> VR_OCC_LOG, c)));
+  const int b = wave_min2(pk2(min(lo[2] >> VR_OCC_LOG, c), min(-(hi[0] >> VR_OCC_LOG), c)));
+  const int d = wave_min2(pk2(min(-(hi[1] >> VR_OCC_LOG), c), min(-(hi[2] >> VR_OCC_LOG), c)));
   const int bx = pk_lo(a), by = pk_hi(a), bz = pk_lo(b);
   const int cx = -pk_hi(b) - bx + 1, cy = -pk_lo(d) - by + 1, cz = -pk_hi(d) - bz + 1;
   if (cx <= 0 || cy <= 0 || cz <= 0) return 1;  // no live ray
