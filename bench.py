@@ -335,6 +335,10 @@ def main():
                          "kernels_timed": timed_kernels,
                          "bytes_per_launch": bytes_launch,
                          "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F,
+                         "note": "SURVEY 8d's definitional sample-stream bytes: every sample charged F fetches, "
+                                 "but opacity-0 samples (60.5 %% at the metric config) are leaped or skip their "
+                                 "shading, so frac can exceed 1; the hardware fractions are in `binding` "
+                                 "(DESIGN.md s7)",
                          "fetched": {"bytes_per_launch": fetched,
                                      "achieved": round(fetched / t_kernel_s / 1e9, 1),
                                      "frac": round(fetched / t_kernel_s / 1e9 / HBM_PEAK_GBS, 4),

@@ -347,6 +347,16 @@ bool env_flag_off(const char *name) {
   const char *ev = std::getenv(name);
   return ev && ev[0] == '0';
 }
+// A/B and diagnostic switches (INTEGRATION.md "Runtime switches"): read by a DIAG=1 build only
+// (Makefile; -DVR_DIAG=1), ignored by the default library
+#ifndef VR_DIAG
+#define VR_DIAG 0
+#endif
+const char *diag_env(const char *name) { return VR_DIAG ? std::getenv(name) : nullptr; }
+bool diag_flag(const char *name) {
+  const char *ev = diag_env(name);
+  return ev && ev[0] == '1';
+}
 
 // syncVolume (kernel.cu:659-672): unbind the texture, drop the old array, upload the volume into a
 // device buffer and bind it.  The handle's previous buffer of the slot is rewritten in place when
@@ -359,7 +369,7 @@ bool env_flag_off(const char *name) {
 void build_zpair(DevBuf *b, hipStream_t s) {
   const uint64_t padded = (b->dims[0] + 2) * (b->dims[1] + 2) * (b->dims[2] + 2);
   const bool want = padded < (1ull << 22) && !(b->dims[0] == 1 && b->dims[1] == 1 && b->dims[2] == 1) &&
-                    !env_flag("VR_NO_ZPAIR");
+                    !diag_flag("VR_NO_ZPAIR");
   if (!want) {
     if (b->zpair) vr_host::pooled_free(b->zpair, b->zpair_bytes, b->device, vr_host::Readers(b->readers));
     b->zpair = nullptr;
@@ -787,14 +797,14 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
     const double xe = std::fabs((double)P.fe) * vmax(eb) * (double)P.tstep;
     P.small_x = (std::isfinite(xa) && xa < 0x1p-7 * 0.999) ? 1 : 0;
     P.eds_finite = (std::isfinite(xe) && xe < 1e38) ? 1 : 0;
-    if (env_flag("VR_NO_RANGE_FLAGS")) P.small_x = P.eds_finite = 0;  // A/B and test switch
+    if (diag_flag("VR_NO_RANGE_FLAGS")) P.small_x = P.eds_finite = 0;  // A/B switch (DIAG build)
   }
   {
     const bool re_ok = P.re_is_em || (P.re.p && P.re.one);
     const bool lut_ok = g_tex.lights.empty() || (P.lut.p && P.lut.small && !P.lut.one && P.lut.zp);
     // (tstep > 0: the march's t only grows, which advance_k relies on)
     const bool step_ok = std::isfinite(P.tstep) && P.tstep > 0.f;
-    P.tame = (P.skip_empty && P.eds_finite && P.small_x && re_ok && lut_ok && step_ok && !env_flag("VR_NO_TAME")) ? 1
+    P.tame = (P.skip_empty && P.eds_finite && P.small_x && re_ok && lut_ok && step_ok && !diag_flag("VR_NO_TAME")) ? 1
                                                                                                             : 0;
     P.re_mask = P.re_is_em ? 0xffffffffu : 0u;
   }
@@ -1035,7 +1045,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     uint32_t every = VR_SCHED_REMEASURE;
     if (const char *ev = std::getenv("VR_SCHED_REMEASURE")) every = (uint32_t)std::max(1, std::atoi(ev));
     uint32_t heavy_div = VR_SCHED_HEAVY_DIV;
-    if (const char *ev = std::getenv("VR_SCHED_HEAVY_DIV")) heavy_div = (uint32_t)std::max(1, std::atoi(ev));
+    if (const char *ev = diag_env("VR_SCHED_HEAVY_DIV")) heavy_div = (uint32_t)std::max(1, std::atoi(ev));
     uint32_t tail_pct = VR_SCHED_TAIL_PCT;
     if (const char *ev = std::getenv("VR_SCHED_TAIL_PCT")) tail_pct = (uint32_t)std::max(0, std::atoi(ev));
     if (!S.h_cost) {
@@ -1049,12 +1059,12 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
     }
     // VR_SCHED_ROWS=1 (A/B): tile rows of workgroups in the order of their heaviest block, each row
     // in its own order -- the heavy band early, row-major neighbours still together
-    const bool rows = env_flag("VR_SCHED_ROWS");
+    const bool rows = diag_flag("VR_SCHED_ROWS");
     // VR_SCHED_SHIFT=r: row-major order with each block moved ahead by r block rows times its
     // duration over the longest block's -- the heavy blocks start early enough to finish with the
     // frame, row-major neighbours stay together (L2), and the frame ends on light blocks
     double shift = VR_SCHED_SHIFT;
-    if (const char *ev = std::getenv("VR_SCHED_SHIFT")) shift = std::max(0.0, std::atof(ev));
+    if (const char *ev = diag_env("VR_SCHED_SHIFT")) shift = std::max(0.0, std::atof(ev));
     if (rows) shift = 0.0;
     if (S.copy_pending && vr_host::query_done(S.copied, "hipEventQuery (schedule durations)")) {  // arrived
       S.copy_pending = false;
@@ -1131,7 +1141,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   // the first round of workgroups (the longest ones) at raised wave priority (A/B: VR_PRIO_BLOCKS);
   // none for a full frame, whose first blocks are only the heavy ones
   P.prio_blocks = P.sched_full ? 0u : (uint32_t)(device_wave_slots() / 4);
-  if (const char *ev = std::getenv("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
+  if (const char *ev = diag_env("VR_PRIO_BLOCKS")) P.prio_blocks = (uint32_t)std::atoi(ev);
   return hipSuccess;
 }
 
