@@ -956,15 +956,15 @@ int depth_lanes(const vr::RenderParams &P) {
 
 // texels a pixel spans at the volume, tau = dist * vw / (W * f) (pixel pitch 2/W on the image plane
 // at f, box x-extent 2 = vw texels), and the wave slot size it asks for at the launch's depth lanes:
-// 12 KiB slots once the hull of a 4x8 tile (K <= 2) passes tau 1.5 (tau 2.0: 18 % faster than
-// 6.5 KiB), of a 4x4 tile (K = 4) tau 3 (tau 2.0 at K = 4: 19.5 ms with 6.5 KiB slots, 20.7 with
-// 12 KiB).  VR_WIDE_SLOT=0/1 overrides (A/B).
+// 12 KiB slots once the hull of a wave's tile passes tau 1.5 (K <= 2, tau 2.0: 18 % faster than
+// 6.5 KiB; K = 4 since round 5, below).  VR_WIDE_SLOT=0/1 overrides (A/B).
 void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
   const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
   const double tau = (f > 0 && P.width > 0) ? dist * vw / ((double)P.width * f) : 1e30;
   P.tau = (float)std::min(tau, 1e30);
-  const int K = P.steps ? 1 : depth_lanes(P);
-  P.wide_slot = tau > (K >= 4 ? 3.0 : 1.5) ? 1 : 0;
+  // (round 5: with the empty-space probe the wide slots win at K = 4 too -- C2, tau 2.0: 12.18-12.20
+  // vs 13.13 ms, r5p; round 4 measured the opposite, 20.7 vs 19.5 ms, when every empty chunk staged)
+  P.wide_slot = tau > 1.5 ? 1 : 0;
   if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
 }
 
@@ -1196,7 +1196,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
   // XCD runs of 16 blocks for lookup-gradient frames (their gathers of the gradient copy are the
   // launch's HBM traffic: C3 36.4 -> 35.7 ms, round 4); the compute-gradient march is indifferent
-  P.xcd_run = F.mode == 2 ? 16 : VR_XCD_RUN;
+  P.xcd_run = F.mode == 2 ? 32 : VR_XCD_RUN;  // (round 5: 32 / 16 -> 31.24-31.26 / 31.43-31.67 ms, r5p)
   if (const char *ev = std::getenv("VR_XCD_RUN")) P.xcd_run = std::max(0, std::atoi(ev));  // A/B switch
   P.block_rot = 0;  // set at the launch (block rows of the launch's depth lanes)
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
