@@ -383,7 +383,8 @@ def test_kernel_variants_are_bit_identical(monkeypatch, counter_clock, scene, sh
     for name, env in [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),
                       ("plain_noskip", {"VR_NO_LDS": "1", "VR_NO_EMPTY_SKIP": "1"}), ("tiles1", {"VR_TILE_MODE": "1"}),
                       ("big", {"VR_FORCE_BIG": "1"}), ("plain_big", {"VR_NO_LDS": "1", "VR_FORCE_BIG": "1"}),
-                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"}), ("nogvec", {"VR_NO_GVEC": "1"}),
+                      ("lut_general", {"VR_NO_SMALL_LUT": "1"}), ("wide", {"VR_WIDE_SLOT": "1"}), ("narrow", {"VR_WIDE_SLOT": "0"}),
+                      ("nogvec", {"VR_NO_GVEC": "1"}),
                       ("k1", {"VR_DEPTH_LANES": "1"}), ("k2", {"VR_DEPTH_LANES": "2"}), ("k4", {"VR_DEPTH_LANES": "4"}),
                       ("k8", {"VR_DEPTH_LANES": "8"}), ("k2_noskip", {"VR_DEPTH_LANES": "2", "VR_NO_EMPTY_SKIP": "1"}),
                       ("k8_wide", {"VR_DEPTH_LANES": "8", "VR_WIDE_SLOT": "1"}),
@@ -625,6 +626,7 @@ def test_paired_stereo_tiles_equal_two_renders(monkeypatch, counter_clock, k):
     (none, odd, wider than the image)."""
     from volume_renderer_amd import mex
     monkeypatch.setenv("VR_DEPTH_LANES", k)
+    monkeypatch.setenv("VR_WIDE_SLOT", "0")  # (paired tiles are built for the default slot only)
     v = vr.Volume(O.shell_volume(64))  # a power-of-two cube: the half-texel tap launch
     r = ex1_renderer(v, res=(90, 70), lights=True)
     r.CameraXOffset = 0.5

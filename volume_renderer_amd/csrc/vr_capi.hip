@@ -956,15 +956,20 @@ int depth_lanes(const vr::RenderParams &P) {
 
 // texels a pixel spans at the volume, tau = dist * vw / (W * f) (pixel pitch 2/W on the image plane
 // at f, box x-extent 2 = vw texels), and the wave slot size it asks for at the launch's depth lanes:
-// 12 KiB slots once the hull of a wave's tile passes tau 1.5 (K <= 2, tau 2.0: 18 % faster than
-// 6.5 KiB; K = 4 since round 5, below).  VR_WIDE_SLOT=0/1 overrides (A/B).
+// wide (10 KiB, vr_stage.h) slots once the hull of a wave's tile passes tau 1.5 (K <= 2, tau 2.0:
+// 18 % faster than 6.5 KiB), and for every K = 4 launch (round 5, below).  VR_WIDE_SLOT=0/1 overrides (A/B).
 void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
   const double f = std::fabs((double)a->props[1]), dist = std::fabs((double)a->props[2]);
   const double tau = (f > 0 && P.width > 0) ? dist * vw / ((double)P.width * f) : 1e30;
   P.tau = (float)std::min(tau, 1e30);
-  // (round 5: with the empty-space probe the wide slots win at K = 4 too -- C2, tau 2.0: 12.18-12.20
-  // vs 13.13 ms, r5p; round 4 measured the opposite, 20.7 vs 19.5 ms, when every empty chunk staged)
-  P.wide_slot = tau > 1.5 ? 1 : 0;
+  // Round 5: with the empty-space probe the wide slots win for every K = 4 launch -- C2 (tau 2.0)
+  // 12.18-12.20 vs 13.13 ms at 12 KiB (r5p), 10.90-10.93 ms at 10 KiB (r5u), the P = 8 / P = 4
+  // parts of the metric frame (tau 1.07, short launches) 4.85-4.87 vs 5.26-5.27 / 8.48-8.51 vs
+  // 8.81-8.83 ms (r5s; 10 KiB: 4.82-5.00 / 8.00, r5t-u); at K = 2 they still lose below
+  // tau 1.5 (metric frame 30.2-30.3 vs 26.9-27.0 ms, P = 2 parts 15.15 vs 14.80-14.84 ms).  Round 4
+  // measured the opposite at K = 4 (20.7 vs 19.5 ms at C2), when every empty chunk staged its box.
+  const int K = P.steps ? 1 : depth_lanes(P);
+  P.wide_slot = (tau > 1.5 || K >= 4) ? 1 : 0;
   if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
 }
 

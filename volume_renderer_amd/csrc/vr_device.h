@@ -83,7 +83,7 @@ struct RenderParams {
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)
   int32_t xcd_run;                // march, unscheduled: runs of this many consecutive blocks per XCD (0/1: off)
   uint32_t block_rot;             // march, unscheduled: workgroup b marches block (b + block_rot) mod grid
-  int32_t wide_slot;              // march: 12 KiB wave slots instead of 6 KiB (vr_stage.h)
+  int32_t wide_slot;              // march: 10 KiB wave slots instead of 6.5 KiB (vr_stage.h)
   int32_t fast_shade;             // 1: hardware-rsq shading and exp2 opacity (default); 0: the oracle's ops
   // image-space partition (vr_partition): local column lc -> global column
   int32_t block_cols, part, num_parts, part_cols;

@@ -19,7 +19,10 @@ namespace vr {
 #define VR_LDS_CAP 1664        // 6.5 KiB: 26 KiB per workgroup -> 6 workgroups (24 waves) per CU
 #endif
 #ifndef VR_LDS_CAP_WIDE
-#define VR_LDS_CAP_WIDE 3072   // 12 KiB: 3 workgroups per CU, for footprints above ~1.5 texels/pixel
+// 10 KiB: 4 workgroups per CU, for footprints above ~1.5 texels/pixel and every K = 4 launch (round 5:
+// 2560 instead of 3072 floats -- C2 12.23 -> 10.93-10.97 ms, P = 8 part 4.89-4.93 -> 4.82-4.87, r5t;
+// 2304 / 2048 floats: C2 11.18-11.22 / 11.88-11.93 ms, P = 4 part 8.25 / 8.33 vs 8.00, r5u)
+#define VR_LDS_CAP_WIDE 2560
 #endif
 #ifndef VR_STAGE_UNROLL
 #define VR_STAGE_UNROLL 4  // loads in flight per lane while staging
