@@ -17,7 +17,8 @@ Steps ('|' separates variants, ',' environment assignments inside a variant):
   bench[:ARGS]                   the bench line (CPU baseline included unless ARGS say otherwise)
                                  -> bench.json (the N-th bench step of a pass: benchN.json)
   kt[:ARGS]                      rocprofv3 --kernel-trace --stats of bench.py      -> ktN/ (N-th kt)
-  pmc[:ARGS]                     tools/pmc.sh counter passes (one group per pass)  -> pmcN/ (N-th pmc)
+  pmc[:[@K=V,..@]ARGS]           tools/pmc.sh counter passes (one group per pass)  -> pmcN/ (N-th pmc);
+                                 @..@ sets the environment (e.g. VR_LIB_PATH of a variant)
   py:SCRIPT[ ARGS]               any python script of the tree (e.g. tools/tail_profile.py ...)
 """
 import json
@@ -131,8 +132,13 @@ def main():
                      env=e)
         elif kind == "pmc":
             n_pmc += 1
+            penv = None
+            if rest.startswith("@"):  # pmc:@K=V,K=V@ ARGS -- environment of the profiled runs
+                spec, _, rest = rest[1:].partition("@")
+                penv = dict(os.environ)
+                penv.update(parse_env(spec))
             rc = run(["bash", "tools/pmc.sh", os.path.join(out, f"pmc{n_pmc}")] + shlex.split(rest),
-                     os.path.join(out, f"pmc{n_pmc}.log"), 1000)
+                     os.path.join(out, f"pmc{n_pmc}.log"), 1000, env=penv)
         elif kind == "py":
             rc = run([PY, "-u"] + shlex.split(rest), os.path.join(out, "py.log"), 900)
         else:

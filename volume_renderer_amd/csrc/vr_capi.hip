@@ -76,8 +76,9 @@ hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int3
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
 hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, hipStream_t s);
-hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n,
-                              hipStream_t s);
+uint64_t interleave3_entries(uint32_t px, uint32_t py, uint32_t pz);
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint32_t px,
+                              uint32_t py, uint32_t pz, hipStream_t s);
 hipError_t launch_sum_channels(const float *in, uint32_t nch, uint32_t nv, uint64_t img, float *out, hipStream_t s);
 hipError_t launch_assemble(const float *parts, int64_t w, int64_t h, int32_t bc, int32_t np,
                            int64_t max_cols, float *out, hipStream_t s);
@@ -1226,19 +1227,20 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     // gathers from three volumes); without memory for it the kernel gathers them separately
     const BufPtr &bx = g_tex.bind[T_DX], &by = g_tex.bind[T_DY], &bz = g_tex.bind[T_DZ];
     TexUnit::GVec &G = g_tex.gvec[h->device];
+    const uint32_t gpx = P.gx.px, gpy = P.gx.pxy / P.gx.px, gpz = (uint32_t)P.gx.nz + 2u;
     bool fresh = G.buf != nullptr;
     const DevBuf *src[3] = {bx.get(), by.get(), bz.get()};
     for (int i = 0; i < 3 && fresh; ++i) fresh = G.src[i] == src[i] && G.ver[i] == src[i]->version;
     if (!fresh) {
       G.buf.reset();
-      const uint64_t n = bx->bytes / sizeof(float);
+      const uint64_t n = vr::interleave3_entries(gpx, gpy, gpz);
       auto gv = std::make_shared<DevBuf>();
       gv->device = h->device;
       gv->bytes = n * 4 * sizeof(float);
       const hipError_t ea = vr_host::pooled_alloc(reinterpret_cast<void **>(&gv->ptr), gv->bytes, h->device);
       if (ea == hipSuccess) {
         for (const BufPtr *b : {&bx, &by, &bz}) wait_ready(*b, stream);
-        VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, n, stream));
+        VR_HIP(vr::launch_interleave3(bx->ptr, by->ptr, bz->ptr, gv->ptr, gpx, gpy, gpz, stream));
         // launches on other streams (another handle, a group's other children on this device) find
         // the copy fresh and wait for this event before reading it (bind_reads)
         VR_HIP(vr_host::record_event(stream, gv->ready));
@@ -1252,7 +1254,11 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
         gv->ptr = nullptr;
       }
     }
-    if (G.buf) P.gvec = G.buf->ptr;
+    if (G.buf) {
+      P.gvec = G.buf->ptr;
+      P.gv_row8 = 8u * ((gpx + 1) >> 1);
+      P.gv_plane8 = P.gv_row8 * ((gpy + 1) >> 1);
+    }
   }
   if (fusable && march && F.mode <= 1 && !F.big && !P.steps) {
     *fusable = 1;

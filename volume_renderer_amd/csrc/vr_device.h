@@ -36,6 +36,13 @@ struct DevTex {
 #define VR_OCC_LOG 3
 #endif
 
+// Layout of the interleaved lookup gradient (RenderParams::gvec): 1 -- 2x2x2 bricks of padded
+// voxels, one 128-byte line each (vr_kernels.hip interleave3_kernel, vr_sampling.h fetch_vec);
+// 0 -- rows of the padded volume.
+#ifndef VR_GVEC_BRICK
+#define VR_GVEC_BRICK 1
+#endif
+
 // One light in kernel order (position reversed from MATLAB, render.cpp:167-168).
 struct DevLight {
   float px, py, pz;
@@ -70,6 +77,7 @@ struct RenderParams {
   const DevLight *lights;
   DevTex em, ab, re, gem, gx, gy, gz, lut;
   const float *gvec;              // lookup gradient interleaved, (gx, gy, gz, 0) per padded voxel, or null
+  uint32_t gv_row8, gv_plane8;    // VR_GVEC_BRICK: entries per row / plane of 2x2x2 bricks (vr_sampling.h)
   int32_t re_is_em;               // reflection texture == emission texture (sample reused)
   int32_t skip_empty;             // alpha == 0 samples may skip shading (exactly 0 contribution)
   int32_t small_x;                // every |Fa * ab(p) * tstep| < 2^-7: opacity without a range test

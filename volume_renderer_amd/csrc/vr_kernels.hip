@@ -387,22 +387,47 @@ hipError_t launch_gradient(const float *d, const uint64_t dims[3], float *gx, fl
   return hipGetLastError();
 }
 
+// out[e] = (a, b, c, 0) of padded voxel e: rows of the padded volume, or (VR_GVEC_BRICK) 2x2x2
+// bricks, entry ((Z/2 * by + Y/2) * bx + X/2) * 8 + (X&1) + 2 (Y&1) + 4 (Z&1) (vr_sampling.h
+// fetch_vec), the bricks past an odd padded edge zero-filled.
 __global__ __launch_bounds__(256) void interleave3_kernel(const float *__restrict__ a, const float *__restrict__ b,
                                                           const float *__restrict__ c, float4 *__restrict__ out,
-                                                          uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = make_float4(a[i], b[i], c[i], 0.f);
+                                                          uint64_t n, uint32_t px, uint32_t py, uint32_t pz) {
+  const uint32_t bx = (px + 1) >> 1, by = (py + 1) >> 1;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t src = i;
+    if (VR_GVEC_BRICK) {
+      const uint64_t brick = i >> 3, e = i & 7u;
+      const uint64_t bz = brick / ((uint64_t)bx * by), rem = brick - bz * bx * by;
+      const uint32_t byi = (uint32_t)(rem / bx), bxi = (uint32_t)(rem - (uint64_t)byi * bx);
+      const uint32_t X = 2u * bxi + (uint32_t)(e & 1u), Y = 2u * byi + (uint32_t)((e >> 1) & 1u);
+      const uint64_t Z = 2u * bz + (e >> 2);
+      if (X >= px || Y >= py || Z >= pz) {
+        out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
+      src = (Z * py + Y) * px + X;
+    }
+    out[i] = make_float4(a[src], b[src], c[src], 0.f);
+  }
 }
 
-// out: n entries (gx, gy, gz, 0) of the interleaved lookup gradient (RenderParams::gvec).  (Round 4
-// also measured a z-paired and a packed 12-byte layout, both slower; removed in round 5.)
-hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint64_t n,
-                              hipStream_t s) {
+// Entries of the interleaved lookup gradient of a padded px x py x pz volume.
+uint64_t interleave3_entries(uint32_t px, uint32_t py, uint32_t pz) {
+  if (!VR_GVEC_BRICK) return (uint64_t)px * py * pz;
+  return 8ull * ((px + 1) >> 1) * ((py + 1) >> 1) * ((pz + 1) >> 1);
+}
+
+// out: interleave3_entries entries (gx, gy, gz, 0) of the lookup gradient (RenderParams::gvec).
+// (Round 4 also measured a z-paired and a packed 12-byte layout, both slower; removed in round 5.)
+hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint32_t px,
+                              uint32_t py, uint32_t pz, hipStream_t s) {
+  const uint64_t n = interleave3_entries(px, py, pz);
   if (!n) return hipSuccess;
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 262144) blocks = 262144;
   hipLaunchKernelGGL(interleave3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, c,
-                     reinterpret_cast<float4 *>(out), n);
+                     reinterpret_cast<float4 *>(out), n, px, py, pz);
   return hipGetLastError();
 }
 

@@ -335,7 +335,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     } else if (MODE == 2 && SHARE2) {
       const Ax cx = clamp_ax(ax, E.nx), cy = clamp_ax(ay, E.ny), cz = clamp_ax(az, E.nz);
       if (P.gvec)
-        g = fetch_vec<BIG>(P.gvec, P.gx, cx, cy, cz);
+        g = fetch_vec<BIG>(P.gvec, P.gx, P.gv_row8, P.gv_plane8, cx, cy, cz);
       else
         g = mk(fetch<BIG>(P.gx, cx, cy, cz), fetch<BIG>(P.gy, cx, cy, cz), fetch<BIG>(P.gz, cx, cy, cz));
     } else {

@@ -283,16 +283,33 @@ __device__ __forceinline__ float lut_light(const DevTex &lut, const AxF &la, flo
 }
 
 // Trilinear fetch of the three lookup-gradient textures at once from their interleaved copy
-// (RenderParams::gvec, pitches of `t`): per row the x-pair is two aligned 16-byte loads, and each
-// component goes through exactly the interpolation fetch() applies to its own texture.
+// (RenderParams::gvec): eight aligned 16-byte corner loads, and each component goes through exactly
+// the interpolation fetch() applies to its own texture.  VR_GVEC_BRICK: padded voxel (X, Y, Z) is
+// entry ((Z/2 * by + Y/2) * bx + X/2) * 8 + (X&1) + 2 (Y&1) + 4 (Z&1) -- a cell's corners span
+// 1-8 lines (3.4 on average) where rows of the padded volume take 4-8 (4.5), and a wave's oblique
+// footprint touches fewer lines.  Without it: rows of the padded volume (pitches of `t`).
 template <bool BIG>
-__device__ __forceinline__ f3 fetch_vec(const float *gvec, const DevTex &t, const Ax &ax, const Ax &ay, const Ax &az) {
-  uint64_t o;
-  if (BIG) o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
-  else o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
-  const float4 *b = reinterpret_cast<const float4 *>(gvec) + o;
-  const float4 a00 = b[0], b00 = b[1], a10 = b[t.px], b10 = b[t.px + 1];
-  const float4 a01 = b[t.pxy], b01 = b[t.pxy + 1], a11 = b[t.pxy + t.px], b11 = b[t.pxy + t.px + 1];
+__device__ __forceinline__ f3 fetch_vec(const float *gvec, const DevTex &t, uint32_t row8, uint32_t plane8,
+                                        const Ax &ax, const Ax &ay, const Ax &az) {
+  float4 a00, b00, a10, b10, a01, b01, a11, b11;
+  if (VR_GVEC_BRICK) {
+    const uint32_t X = (uint32_t)(ax.i + 1), Y = (uint32_t)(ay.i + 1), Z = (uint32_t)(az.i + 1);
+    const uint32_t dx = (X & 1u) ? 7u : 1u, dy = (Y & 1u) ? row8 - 2u : 2u, dz = (Z & 1u) ? plane8 - 4u : 4u;
+    const uint32_t xy = ((X >> 1) << 3) + (X & 1u) + (Y >> 1) * row8 + ((Y & 1u) << 1) + ((Z & 1u) << 2);
+    uint64_t o;
+    if (BIG) o = (uint64_t)(Z >> 1) * plane8 + xy;
+    else o = (Z >> 1) * plane8 + xy;
+    const float4 *b = reinterpret_cast<const float4 *>(gvec) + o;
+    a00 = b[0], b00 = b[dx], a10 = b[dy], b10 = b[dy + dx];
+    a01 = b[dz], b01 = b[dz + dx], a11 = b[dz + dy], b11 = b[dz + dy + dx];
+  } else {
+    uint64_t o;
+    if (BIG) o = ((uint64_t)(az.i + 1) * t.pxy + (uint64_t)(ay.i + 1) * t.px) + (uint64_t)(ax.i + 1);
+    else o = ((uint32_t)(az.i + 1) * t.pxy + (uint32_t)(ay.i + 1) * t.px) + (uint32_t)(ax.i + 1);
+    const float4 *b = reinterpret_cast<const float4 *>(gvec) + o;
+    a00 = b[0], b00 = b[1], a10 = b[t.px], b10 = b[t.px + 1];
+    a01 = b[t.pxy], b01 = b[t.pxy + 1], a11 = b[t.pxy + t.px], b11 = b[t.pxy + t.px + 1];
+  }
   f3 r;
 #define VR_TRI(c)                                                                                  \
   {                                                                                                \
