@@ -1230,6 +1230,7 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
 // ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation and the matching
 // sort-last slab kernel, for a quick look at their code without compiling every variant.
 template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);
+template __global__ void march_kernel<2, 2, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);  // C3
 template __global__ void march_slab_kernel<2, 1, true, VR_LDS_CAP, false>(const RenderParams P);
 #endif  // !VR_ISA_PROBE
 }  // namespace fast / exact
