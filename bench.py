@@ -47,6 +47,15 @@ def workload_name(n, W, H, L, gradient):
             + ", rotate(125,25,0) f=3 dist=6 thr=0.9")
 
 
+def launched_lanes(timed_kernels):
+    """Depth lanes K of the march kernel the timed frames launched (its first template argument)."""
+    if not timed_kernels:
+        return None
+    name = max(timed_kernels, key=timed_kernels.get)
+    head = name.split("march_kernel<", 1)
+    return int(head[1].split(",", 1)[0]) if len(head) == 2 else None
+
+
 def rotation(alpha, beta, gamma):
     """VolumeRender.rotate from identity (exact cosd/sind at multiples of 90)."""
     from volume_renderer_amd.volume_render import _cosd, _sind
@@ -318,7 +327,8 @@ def main():
                        "volume": [n, n, n], "image": [W, H], "lights": L, "gradient": args.gradient,
                        "parallelism": f"image-column partition x{world} (block {args.block_cols})"
                        + (" + RCCL gather" if world > 1 else ""),
-                       "depth_lanes": mex.depth_lanes(my_cols, H, 6.0 * n / (W * 3.0)),  # dist * n / (W * f)
+                       "depth_lanes": launched_lanes(timed_kernels)
+                       or mex.depth_lanes(my_cols, H, 6.0 * n / (W * 3.0)),  # dist * n / (W * f)
                        "frames": "serial, one HIP stream"},
             "samples_per_frame": total_samples,
             "shaded_samples_per_frame": total_lit,
@@ -336,7 +346,7 @@ def main():
                          "bytes_per_launch": bytes_launch,
                          "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F,
                          "note": "SURVEY 8d's definitional sample-stream bytes: every sample charged F fetches, "
-                                 "but opacity-0 samples (60.5 %% at the metric config) are leaped or skip their "
+                                 "but opacity-0 samples (60.5 % at the metric config) are leaped or skip their "
                                  "shading, so frac can exceed 1; the hardware fractions are in `binding` "
                                  "(DESIGN.md s7)",
                          "fetched": {"bytes_per_launch": fetched,

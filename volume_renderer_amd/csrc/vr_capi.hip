@@ -950,6 +950,10 @@ int depth_lanes(const vr::RenderParams &P) {
   const double waves = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0);  // at K = 1
   const double rounds = waves / device_wave_slots();
   const double tau = P.tau > 0.f ? (double)P.tau : 1.0;
+  // a lookup-gradient frame: K = 4, whose four consecutive samples per ray gather mostly the same
+  // corner lines of the gradient copy -- C3 (tau 1.07, 7.9 rounds) 27.90-27.99 ms with 6.5 KiB slots
+  // vs 28.87-28.94 at K = 2 (r5z); K = 4 with 10 KiB slots 29.8, K = 1 52.4 (r5y)
+  if (P.lookup) return 4;
   if (rounds < VR_DEPTH_ROUNDS_K2 || tau >= VR_DEPTH_TAU_K4) return 4;
   if (rounds >= VR_DEPTH_ROUNDS_K1 && tau < VR_DEPTH_TAU_K1) return 1;
   return 2;
@@ -970,7 +974,7 @@ void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
   // tau 1.5 (metric frame 30.2-30.3 vs 26.9-27.0 ms, P = 2 parts 15.15 vs 14.80-14.84 ms).  Round 4
   // measured the opposite at K = 4 (20.7 vs 19.5 ms at C2), when every empty chunk staged its box.
   const int K = P.steps ? 1 : depth_lanes(P);
-  P.wide_slot = (tau > 1.5 || K >= 4) ? 1 : 0;
+  P.wide_slot = (tau > 1.5 || (K >= 4 && !P.lookup)) ? 1 : 0;  // (lookup frames: r5y above)
   if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
 }
 
@@ -1195,6 +1199,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   P.out = d_out;
   P.steps = d_steps;
   P.tile_mode = 0;
+  P.lookup = F.mode == 2 ? 1 : 0;
   set_tau_and_slot(P, a, (double)h->vol[T_EM].dims[0]);  // depth lanes and wave slot size
   // shading arithmetic: hardware rsq / exp2 by default; VR_EXACT_SHADE=1 selects
   // the oracle's correctly rounded op sequence (bit-identical to oracle/vr_oracle.c up to acosf)

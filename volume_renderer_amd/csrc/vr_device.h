@@ -88,6 +88,7 @@ struct RenderParams {
   int32_t tame;
   uint32_t re_mask;               // tame: ~0 if the reflection sample is the emission sample, else 0
   float tau;                      // host only: texels a pixel spans at the volume (depth_lanes)
+  int32_t lookup;                 // host only: a lookup-gradient frame (depth_lanes, wave slot)
   int32_t tile_mode;              // 0: row-major tiles, 1: XCD-aware super-tiles (general kernel)
   int32_t xcd_run;                // march, unscheduled: runs of this many consecutive blocks per XCD (0/1: off)
   uint32_t block_rot;             // march, unscheduled: workgroup b marches block (b + block_rot) mod grid
