@@ -280,6 +280,12 @@ struct vr_context {
   bool peer = true;
   float *d_part = nullptr;        // child: its part image; primary: all parts
   size_t d_part_bytes = 0;
+  // child without a peer mapping: the pinned staging buffer of its part gather, kept across frames
+  // (the gather's D2H waits for the previous frame's assembly, so the last H2D has read it), and the
+  // completion of the last H2D that read it
+  void *pin = nullptr;
+  size_t pin_bytes = 0;
+  vr_host::EventPtr pin_read;
   // the last launch's kernel time on this context's device (events around the march launch of
   // do_render / a fused channel launch), reported by mem_info; created on first use
   hipEvent_t tev[2] = {nullptr, nullptr};
@@ -1473,12 +1479,22 @@ int do_render_slab(vr_context *h, const vr_render_args *a, const vr_slab *sl, co
 
 // A device-to-device copy through pinned host memory, for device pairs without a peer mapping: the
 // D2H is issued on `ss` (a stream of sdev) -- synchronously when ss is null --, the H2D on `ds` (a
-// stream of ddev) after it; the pinned buffer is released when the H2D has completed.  Returns the
-// completion event of the H2D.
+// stream of ddev) after it.  Through the caller's pinned buffer `stage` (which the caller keeps
+// until the H2D has completed), or through one allocated here and released when the H2D has
+// completed (or at once if a call fails).  Returns the completion event of the H2D.
 vr_host::EventPtr staged_copy(void *dst, int ddev, hipStream_t ds, const void *src, int sdev, hipStream_t ss,
-                              size_t bytes) {
-  void *pin = nullptr;
-  VR_HIP(hipHostMalloc(&pin, bytes, hipHostMallocDefault));
+                              size_t bytes, void *stage = nullptr) {
+  struct Own {  // the buffer allocated here, freed on an error path
+    void *p = nullptr;
+    ~Own() {
+      if (p) (void)hipHostFree(p);
+    }
+  } own;
+  void *pin = stage;
+  if (!pin) {
+    VR_HIP(hipHostMalloc(&own.p, bytes, hipHostMallocDefault));
+    pin = own.p;
+  }
   vr_host::EventPtr e1, e2;
   {
     DeviceGuard g(sdev);
@@ -1493,7 +1509,10 @@ vr_host::EventPtr staged_copy(void *dst, int ddev, hipStream_t ds, const void *s
   if (e1) VR_HIP(hipStreamWaitEvent(ds, e1->e, 0));
   VR_HIP(hipMemcpyAsync(dst, pin, bytes, hipMemcpyHostToDevice, ds));
   VR_HIP(vr_host::record_event(ds, e2));
-  vr_host::free_when_done(pin, ddev, vr_host::readers_of(e2), true);
+  if (own.p) {
+    vr_host::free_when_done(own.p, ddev, vr_host::readers_of(e2), true);
+    own.p = nullptr;
+  }
   return e2;
 }
 
@@ -1633,10 +1652,21 @@ void group_gather_assemble(vr_context *h, int nviews, size_t part_floats, int64_
                                   c->d_part + (size_t)v * part_floats, c->device, part_floats * sizeof(float),
                                   c->gstream));
     } else {  // no peer mapping: D2H on the child's stream, H2D on the primary's (after the previous
-              // frame's assembly, which read these slots, in that stream's order)
+              // frame's assembly, which read these slots, in that stream's order), through the
+              // child's persistent pinned buffer (its previous contents read by that assembly's H2Ds)
+      const size_t vb = part_floats * sizeof(float);
+      if (c->pin_bytes < (size_t)nviews * vb) {
+        if (c->pin) vr_host::free_when_done(c->pin, c->device, vr_host::readers_of(c->pin_read), true);
+        c->pin = nullptr;
+        c->pin_bytes = 0;
+        c->pin_read.reset();
+        VR_HIP(hipHostMalloc(&c->pin, (size_t)nviews * vb, hipHostMallocDefault));
+        c->pin_bytes = (size_t)nviews * vb;
+      }
       for (int v = 0; v < nviews; ++v)
-        (void)staged_copy(h->d_part + ((size_t)v * n + k) * part_floats, h->device, stream,
-                          c->d_part + (size_t)v * part_floats, c->device, c->gstream, part_floats * sizeof(float));
+        c->pin_read = staged_copy(h->d_part + ((size_t)v * n + k) * part_floats, h->device, stream,
+                                  c->d_part + (size_t)v * part_floats, c->device, c->gstream, vb,
+                                  static_cast<char *>(c->pin) + (size_t)v * vb);
     }
     VR_HIP(hipEventRecord(c->gdone, c->gstream));
   }
@@ -1718,6 +1748,8 @@ void delete_children(vr_context *h) {
     for (auto &b : c->buf) b.reset();
     if (c->d_part) (void)hipFree(c->d_part);
     if (c->d_out) (void)hipFree(c->d_out);
+    if (c->pin) vr_host::free_when_done(c->pin, c->device, vr_host::readers_of(c->pin_read), true);
+    c->pin = nullptr;
     free_schedules(c);
     free_views(c);
     if (c->gdone) (void)hipEventDestroy(c->gdone);
