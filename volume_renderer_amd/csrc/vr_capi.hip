@@ -99,10 +99,15 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 #define VR_DEPTH_ROUNDS_K2 3.0   // K = 2 at >= this many, K = 4 below
 #endif
 #ifndef VR_SCHED_HEAVY_DIV
-#define VR_SCHED_HEAVY_DIV 8  // full-frame schedule: heavy = duration >= the longest block's / this
+#define VR_SCHED_HEAVY_DIV 16  // full-frame schedule: heavy = duration >= the longest block's / this
 #endif
 #ifndef VR_SCHED_TAIL_PCT
-#define VR_SCHED_TAIL_PCT 60  // heavy-first only when the longest block >= this % of the packed frame
+// heavy-first only when the longest block >= this % of the packed frame.  Round 5: 0, i.e. every full
+// frame heavy-first -- with the empty-space probe the metric frame's ramp-down (the blocks started
+// last, ~3.5 ms each, 3.9-4.5 ms below 90 % residency, r5ad) outweighs the row-major order's L2
+// locality: 27.50-27.62 -> 26.42-26.51 ms same box (heavy = longest / 16; / 8 26.47-26.62, / 32
+// 26.37-26.64, / 4 26.80-27.17, / 2 28.27-28.82; r5ae, r5af); C3 28.83 -> 28.62, C2 and C5 unchanged
+#define VR_SCHED_TAIL_PCT 0
 #endif
 #ifndef VR_SCHED_SHIFT
 #define VR_SCHED_SHIFT 0.0  // full frames: heavy blocks moved ahead by this many block rows x duration / longest
