@@ -96,6 +96,12 @@ def main():
     ap.add_argument("--chunk-stats-k", action="store_true",
                     help="diagnostic (a VR_COUNT_K=1 build): also the chunk statistics of the production "
                          "depth lanes (the default counted launch runs at K = 1)")
+    ap.add_argument("--gather", choices=["overlap", "serial"], default="overlap",
+                    help="N > 1: frame i's gather to rank 0 overlapped with frame i + 1's render (two part "
+                         "buffers, parallel.FrameGather), or finished before the next frame starts")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (RCCL over xGMI, the product); gloo: a rehearsal of the N > 1 path with every "
+                         "rank on the visible GPUs round-robin (several on one GPU), collectives on host copies")
     ap.add_argument("--traffic-json", default=_latest_traffic_json(),
                     help="PMC-measured HBM bytes per launch of the march kernel (tools/profile_summary.py)")
     args = ap.parse_args()
@@ -106,9 +112,15 @@ def main():
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run --nproc-per-node N")
+    gloo = args.dist_backend == "gloo"
+    if gloo:  # rehearsal: ranks dealt round-robin to the visible GPUs (device_count does not initialise HIP)
+        local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import volume_renderer_amd as vr
     from volume_renderer_amd import mex
@@ -126,7 +138,13 @@ def main():
         mex.synth_shell_device(vol_t.data_ptr(), n, sptr)
     torch.cuda.synchronize(dev)
     from volume_renderer_amd import parallel
-    bcast = parallel.broadcast_volume(vol_t, world, rank) if world > 1 else None
+    if world > 1 and gloo:  # (gloo: through a host copy)
+        vol_h = vol_t.cpu()
+        bcast = parallel.broadcast_volume(vol_h, world, rank)
+        vol_t.copy_(vol_h)
+        del vol_h
+    else:
+        bcast = parallel.broadcast_volume(vol_t, world, rank) if world > 1 else None
     em = mex.DeviceVolume(vol_t.data_ptr(), (n, n, n), last_update=10, owner=vol_t)
     refl = vr.Volume(1)          # VolumeRender.m:131 default VolumeReflection
     refl.TimeLastUpdate = np.uint64(5)
@@ -155,10 +173,17 @@ def main():
     my_cols = mex.partition_columns(W, part)
     max_cols = max(mex.partition_columns(W, mex.partition(args.block_cols, p, world)) for p in range(world)) \
         if world > 1 else W
-    out_local = torch.zeros(3 * max_cols * H, dtype=torch.float32, device=dev)
     full = torch.zeros(3 * W * H, dtype=torch.float32, device=dev) if rank == 0 else None
-    gathered = (torch.zeros(world * 3 * max_cols * H, dtype=torch.float32, device=dev)
-                if (world > 1 and rank == 0) else None)
+    # N > 1: the per-frame gather of the parts to rank 0 and the assembly there (parallel.FrameGather:
+    # two part buffers, frame i's gather overlapped with frame i + 1's render unless --gather serial)
+    fg = None
+    if world > 1:
+        def assemble(gath, _i):
+            mex.assemble_partitions(gath.data_ptr(), W, H, args.block_cols, world, max_cols, full.data_ptr(), sptr)
+        fg = parallel.FrameGather(3 * max_cols * H, world, rank, device=dev, staged=gloo, assemble=assemble)
+        out_local = fg.buffer(0)
+    else:
+        out_local = torch.zeros(3 * max_cols * H, dtype=torch.float32, device=dev)
     steps_t = torch.zeros(48, dtype=torch.int64, device=dev)
 
     # sample count of this rank's launch (exact, counter variant; untimed)
@@ -191,29 +216,30 @@ def main():
                       "global_chunk_box_hist_256": [int(v) for v in steps_t[8:40].tolist()]}
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    # N > 1: the end of each frame's gather (+ assembly on rank 0), for the per-rank attribution
-    evg = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if world > 1 else None
 
     timed_kernels = {}  # march kernel instantiation -> timed frames that launched it
+    nframe = [0]  # frames rendered so far (the part buffer alternates with it at N > 1)
 
     def frame(i=None):
+        k = nframe[0]
+        nframe[0] += 1
+        buf = fg.buffer(k) if fg is not None else out_local
         if i is not None:
             ev[i][0].record(stream)
-        mex.render_device(h, ra, out_local.data_ptr(), part, 0, sptr)
+        mex.render_device(h, ra, buf.data_ptr(), part, 0, sptr)
         if i is not None:
             ev[i][1].record(stream)
             kn = mex.last_march_kernel()
             timed_kernels[kn] = timed_kernels.get(kn, 0) + 1
-        if world > 1:
-            dist.gather(out_local, list(gathered.chunk(world)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                mex.assemble_partitions(gathered.data_ptr(), W, H, args.block_cols, world, max_cols,
-                                        full.data_ptr(), sptr)
-            if i is not None:  # the gather waits on the RCCL stream: this marks its end
-                evg[i].record(stream)
+        if fg is not None:
+            fg.start(k)  # issues this frame's gather, finishes (and on rank 0 assembles) the previous one
+            if args.gather == "serial":
+                fg.flush()
 
     for _ in range(args.warmup):
         frame()
+    if fg is not None:
+        fg.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -221,6 +247,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         frame(i)
+    if fg is not None:
+        fg.flush()  # the last frame's gather and assembly, inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -228,19 +256,27 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     t_kernel_s = sum(kern_ms) / len(kern_ms) / 1e3
+    cdev = torch.device("cpu") if gloo else dev  # device of the small report tensors
     ranks = None
-    if world > 1:  # per-rank kernel and gather + assembly times, all-gathered to rank 0
-        gath_ms = [b.elapsed_time(g) for (_, b), g in zip(ev, evg)]
-        ranks = parallel.rank_report(t_kernel_s * 1e3, sum(gath_ms) / len(gath_ms), world, rank, device=dev)
+    if world > 1:  # per-rank kernel time and the per-frame time beyond it (the exposed gather +
+        # assembly, waiting for the slowest rank included), all-gathered to rank 0
+        exposed = max(0.0, elapsed / args.steps * 1e3 - t_kernel_s * 1e3)
+        ranks = parallel.rank_report(t_kernel_s * 1e3, exposed, world, rank, device=cdev)
+        if ranks is not None:
+            ranks["gather"] = args.gather
+            ranks["what"] = ("mean over the timed frames: march kernel (HIP events around each rank's launch); "
+                             "gather_assembly = the rank's time per frame beyond its kernel (the exposed part of "
+                             "the gather to rank 0 and, on rank 0, of the assembly; waiting for the slowest rank "
+                             "included)")
 
     # ---- extra pass (not `value`): independent frames round-robin on several streams ----------
     pipe_elapsed = None
-    ns = args.pipelined_streams
+    ns = args.pipelined_streams if not (world > 1 and gloo) else 0  # (the rehearsal skips this pass)
     if ns > 1:
         streams = [torch.cuda.Stream(dev) for _ in range(ns)]
         outs = [torch.zeros_like(out_local) for _ in range(ns)]
         fulls = [torch.zeros(3 * W * H, dtype=torch.float32, device=dev) for _ in range(ns)] if rank == 0 else None
-        gaths = ([torch.zeros_like(gathered) for _ in range(ns)] if (world > 1 and rank == 0) else None)
+        gaths = ([torch.zeros_like(fg.gath[0]) for _ in range(ns)] if (world > 1 and rank == 0) else None)
 
         def oframe(i):
             j = i % ns
@@ -287,8 +323,8 @@ def main():
             sim.append(round(e0.elapsed_time(e1) / 3, 3))
         del sim_out
 
-    samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=dev)
-    el = torch.tensor([elapsed, pipe_elapsed or 0.0], dtype=torch.float64, device=dev)
+    samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=cdev)
+    el = torch.tensor([elapsed, pipe_elapsed or 0.0], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(samples_all, op=dist.ReduceOp.SUM)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -329,7 +365,9 @@ def main():
                        + (" + RCCL gather" if world > 1 else ""),
                        "depth_lanes": launched_lanes(timed_kernels)
                        or mex.depth_lanes(my_cols, H, 6.0 * n / (W * 3.0)),  # dist * n / (W * f)
-                       "frames": "serial, one HIP stream"},
+                       "frames": "serial, one HIP stream" + (
+                           "; the gather of frame i overlapped with the render of frame i + 1"
+                           if world > 1 and args.gather == "overlap" else "")},
             "samples_per_frame": total_samples,
             "shaded_samples_per_frame": total_lit,
             "chunks_staged_leaped_global": chunk_stats,
@@ -372,10 +410,12 @@ def main():
             result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
                                              "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
 
-    if rank == 0 and world == 1:  # the frame's identity, also without the CPU baseline (A/B runs)
+    if rank == 0:  # the frame's identity, also without the CPU baseline (A/B runs); at N > 1 the last
+        # frame assembled from the gathered parts -- the same bytes as the one-GPU frame
         import hashlib
+        img = out_local if world == 1 else full
         result["image_sha256"] = hashlib.sha256(
-            np.ascontiguousarray(out_local[: 3 * W * H].view(3, W, H).cpu().numpy()).tobytes()).hexdigest()
+            np.ascontiguousarray(img[: 3 * W * H].view(3, W, H).cpu().numpy()).tobytes()).hexdigest()
 
     # ---- CPU baseline: the oracle's sources at -O3 (C, OpenMP) on a column sample of the frame -----
     if rank == 0 and world == 1 and host_vol is not None:

@@ -176,3 +176,50 @@ def test_partition_layout_covers_every_column_once():
         counts, max_cols = parallel.partition_layout(W, BLOCK, world)
         allc = np.sort(np.concatenate([parallel.partition_column_indices(W, BLOCK, p, world) for p in range(world)]))
         assert np.array_equal(allc, np.arange(W)) and sum(counts) == W and max_cols == counts[0]
+
+
+def _frame_gather_worker(rank, world, port, q, staged):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, frames = 257, 7
+        seen = []
+        fg = parallel.FrameGather(n, world, rank, staged=staged,
+                                  assemble=lambda g, i: seen.append((i, g.clone().numpy())))
+        for i in range(frames):
+            buf = fg.buffer(i)
+            # frame i's "render": a value per (frame, rank, element), written over the buffer of frame i - 2
+            buf.copy_(torch.arange(n, dtype=torch.float32) + 1000.0 * rank + 1e5 * i)
+            fg.start(i)
+            if rank == 0:  # frame i - 1 is assembled once frame i's gather has been issued
+                assert [f for f, _ in seen] == list(range(i))
+        fg.flush()
+        if rank == 0:
+            q.put(seen)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("staged", [False, True])
+def test_frame_gather_overlaps_and_keeps_every_frame(staged):
+    """bench.py's per-frame gather at N > 1 (parallel.FrameGather), over gloo at world 2: frame i's
+    gather is issued after its render and finished (assembled on rank 0) after frame i + 1's render
+    was issued, through two alternating buffers -- every frame reaches rank 0 whole, in order, with
+    each rank's part in rank order, although a buffer is rewritten two frames later; staged: the
+    same through host copies (the one-GPU gloo rehearsal of the bench)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_frame_gather_worker, args=(r, world, port, q, staged)) for r in range(world)]
+    for p in procs:
+        p.start()
+    seen = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [f for f, _ in seen] == list(range(7))
+    n = 257
+    for i, g in seen:
+        want = np.concatenate([np.arange(n, dtype=np.float32) + 1000.0 * r + 1e5 * i for r in range(world)])
+        assert np.array_equal(g, want), i

@@ -38,6 +38,64 @@ def gather_partitions(local, gathered, world: int, rank: int, group=None) -> Non
     dist.gather(local, list(gathered.chunk(world)) if rank == 0 else None, dst=0, group=group)
 
 
+class FrameGather:
+    """The per-frame gather of the column parts to rank 0, overlapped with the next frame's render
+    (bench.py at N > 1): two part buffers per rank (and two gather buffers on rank 0) alternate
+    between frames, so frame i's gather runs on the collective's own stream while frame i + 1
+    renders.  Usage per frame i: render into `buffer(i)` (enqueued on the current stream), then
+    `start(i)`; after the last frame `flush()`.  `start(i)` issues frame i's gather (asynchronous;
+    it waits for the render on the device) and finishes frame i - 1's: the current stream waits for
+    that gather (RCCL; gloo: the host waits), then rank 0 runs `assemble(gathered, frame)` on it.
+    A buffer is written again two frames later, after its gather has been waited for.
+
+    staged=True: for a backend without device-tensor collectives (gloo driving GPU buffers in a
+    rehearsal on one GPU), each part goes through a host copy.  Backend-agnostic otherwise (RCCL on
+    the GPU, gloo on CPU tensors in the test)."""
+
+    def __init__(self, part_numel: int, world: int, rank: int, device=None, dtype=None, staged: bool = False,
+                 assemble=None, group=None):
+        import torch
+        dtype = dtype or torch.float32
+        self.world, self.rank, self.group, self.staged, self.assemble = world, rank, group, staged, assemble
+        self.bufs = [torch.zeros(part_numel, dtype=dtype, device=device) for _ in range(2)]
+        self.gath = ([torch.zeros(world * part_numel, dtype=dtype, device=device) for _ in range(2)]
+                     if rank == 0 else None)
+        if staged:
+            self.hbufs = [torch.zeros(part_numel, dtype=dtype) for _ in range(2)]
+            self.hgath = [torch.zeros(world * part_numel, dtype=dtype) for _ in range(2)] if rank == 0 else None
+        self.pending = None
+
+    def buffer(self, i: int):
+        return self.bufs[i % 2]
+
+    def start(self, i: int) -> None:
+        import torch.distributed as dist
+        slot = i % 2
+        if self.staged:
+            self.hbufs[slot].copy_(self.bufs[slot])  # (synchronous: after the render)
+            src, dst = self.hbufs[slot], self.hgath[slot] if self.rank == 0 else None
+        else:
+            src, dst = self.bufs[slot], self.gath[slot] if self.rank == 0 else None
+        work = dist.gather(src, list(dst.chunk(self.world)) if self.rank == 0 else None, dst=0, group=self.group,
+                           async_op=True)
+        prev, self.pending = self.pending, (work, slot, i)
+        if prev is not None:
+            self._finish(*prev)
+
+    def _finish(self, work, slot: int, i: int) -> None:
+        work.wait()
+        if self.rank == 0:
+            if self.staged:
+                self.gath[slot].copy_(self.hgath[slot])
+            if self.assemble is not None:
+                self.assemble(self.gath[slot], i)
+
+    def flush(self) -> None:
+        if self.pending is not None:
+            prev, self.pending = self.pending, None
+            self._finish(*prev)
+
+
 def volume_checksum(vol):
     """An order-sensitive checksum of a volume's bytes (int64, device-side for a GPU tensor): the sum of
     its 32-bit words weighted by their index mod 65521, plus their plain sum -- equal on two replicas
