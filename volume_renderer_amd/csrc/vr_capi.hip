@@ -1006,11 +1006,14 @@ void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
 // last a whole frame (33 ms of 36 at rotate(30,10,0)) and, started in row-major order, forms a tail
 // the rest of the frame cannot fill.  VR_SCHED=0: no schedule; VR_SCHED_FULL=0: none for full frames.
 bool short_launch(const vr::RenderParams &P) {
-  const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) / device_wave_slots();
+  const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) * std::max(1, (int)P.views) /
+                        device_wave_slots();
   return rounds < VR_SCHED_ROUNDS;
 }
 bool want_schedule(const vr::RenderParams &P) {
-  if (P.views >= 2 || env_flag_off("VR_SCHED")) return false;
+  // fused stereo (two views in one launch, vr_render_stereo) is scheduled over both views' blocks;
+  // not the paired-tile measurement (VR_STEREO_PAIR), nor the multi-view channel kernel
+  if (P.views > 2 || (P.views == 2 && env_flag("VR_STEREO_PAIR")) || env_flag_off("VR_SCHED")) return false;
   return env_flag("VR_SCHED") || short_launch(P) || !env_flag_off("VR_SCHED_FULL");
 }
 
@@ -1027,7 +1030,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
                                     VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
   const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
-  const uint32_t nb = bfns[ki](P);
+  const uint32_t nb = bfns[ki](P) * (uint32_t)std::max(1, (int)P.views);  // (fused stereo: both views' blocks)
   // keyed by stream too: the order buffer of one stream is never rewritten under another's launch
   char key[300];
   std::snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%d/%u/%p/%s", K, P.width, P.height, P.part, P.num_parts,
