@@ -260,3 +260,33 @@ def test_cpu_share_is_positive():
     sys.path.insert(0, ROOT)
     import bench
     assert 1 <= bench.cpu_share() <= (os.cpu_count() or 1)
+
+
+def _gvec_brick_index(X, Y, Z, bx, by):
+    """Entry of padded voxel (X, Y, Z) in the 2x2x2-brick lookup-gradient copy (vr_kernels.hip
+    interleave3_kernel, DESIGN.md s5 "Lookup-gradient copy")."""
+    return (((Z >> 1) * by + (Y >> 1)) * bx + (X >> 1)) * 8 + (X & 1) + 2 * (Y & 1) + 4 * (Z & 1)
+
+
+@pytest.mark.parametrize("dims", [(5, 4, 3), (6, 7, 2), (2, 2, 2), (9, 5, 6)])
+def test_gvec_brick_corner_offsets(dims):
+    """The march's corner addressing in the bricked gradient copy (vr_sampling.h gvec_load): from the
+    cell's first corner (X, Y, Z) the other seven lie at +dx, +dy, +dz and their sums, with dx = 1 or
+    7, dy = 2 or row8 - 2, dz = 4 or plane8 - 4 by the corner's parity -- restated here and checked
+    against the layout for every cell of padded volumes with odd and even edges, and the layout
+    checked to hold every padded voxel once (bricks past an odd edge are padding)."""
+    nx, ny, nz = dims
+    px, py, pz = nx + 2, ny + 2, nz + 2
+    bx, by, bz = (px + 1) // 2, (py + 1) // 2, (pz + 1) // 2
+    row8, plane8 = 8 * bx, 8 * bx * by
+    idx = {(X, Y, Z): _gvec_brick_index(X, Y, Z, bx, by)
+           for X in range(px) for Y in range(py) for Z in range(pz)}
+    assert len(set(idx.values())) == px * py * pz and max(idx.values()) < 8 * bx * by * bz
+    for (X, Y, Z), o in idx.items():
+        if X + 1 >= px or Y + 1 >= py or Z + 1 >= pz:
+            continue
+        dx = 7 if X & 1 else 1
+        dy = row8 - 2 if Y & 1 else 2
+        dz = plane8 - 4 if Z & 1 else 4
+        for cx, cy, cz in itertools.product((0, 1), repeat=3):
+            assert idx[(X + cx, Y + cy, Z + cz)] == o + cx * dx + cy * dy + cz * dz, (X, Y, Z, cx, cy, cz)
