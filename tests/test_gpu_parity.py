@@ -114,6 +114,23 @@ def test_lookup_gradient_then_compute(monkeypatch, counter_clock):
     r.delete()
 
 
+def test_lookup_gradient_odd_padded_edges(monkeypatch, counter_clock):
+    """The bricked lookup-gradient copy (2x2x2 bricks of the padded volume) on a volume
+    whose padded edges are all odd (33 x 21 x 15 -> 35 x 23 x 17): the last brick of every axis is
+    half padding, and every corner of every cell must still read its voxel -- oracle parity per
+    render (harness), as for the cube."""
+    from harness import install
+    install(monkeypatch)
+    v = vr.Volume(np.ascontiguousarray(O.shell_volume(40)[3:36, 9:30, 12:27]))
+    assert tuple(v.Data.shape) == (33, 21, 15)
+    gx, gy, gz = v.grad()
+    r = ex1_renderer(v, res=(72, 64))
+    r.VolumeGradientX, r.VolumeGradientY, r.VolumeGradientZ = gx, gy, gz
+    a = r.render()
+    assert np.isfinite(a).all() and a.max() > 0
+    r.delete()
+
+
 def test_large_illumination_lut(monkeypatch, counter_clock):
     """A LUT of more than 2^22 padded voxels (168^3) takes the general 64-bit-offset LUT fetch
     instead of the fp32-offset one; parity against the oracle as for the 64^3 LUT."""
