@@ -1010,6 +1010,17 @@ bool short_launch(const vr::RenderParams &P) {
                         device_wave_slots();
   return rounds < VR_SCHED_ROUNDS;
 }
+// Very long launches (>= VR_SCHED_LPT_ROUNDS K = 1 waves per wave slot) take the short launches'
+// longest-first schedule as well: C5 (V_shell(2048), 4096^2, 64 rounds) 216.6-217.1 vs 219.1-219.6 ms
+// heavy-first (r5as); the metric frame (7.9 rounds) keeps heavy-first (26.58-26.60 vs 26.32-26.53, r5ae).
+#ifndef VR_SCHED_LPT_ROUNDS
+#define VR_SCHED_LPT_ROUNDS 32.0
+#endif
+bool lpt_launch(const vr::RenderParams &P) {
+  const double rounds = std::ceil(P.part_cols / 8.0) * std::ceil(P.height / 8.0) * std::max(1, (int)P.views) /
+                        device_wave_slots();
+  return rounds < VR_SCHED_ROUNDS || rounds >= VR_SCHED_LPT_ROUNDS;
+}
 bool want_schedule(const vr::RenderParams &P) {
   // fused stereo (two views in one launch, vr_render_stereo) is scheduled over both views' blocks;
   // not the paired-tile measurement (VR_STEREO_PAIR), nor the multi-view channel kernel
@@ -1050,7 +1061,7 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   }
   if (!(S.d_cost && S.blocks == nb)) return hipSuccess;
   hipError_t rc = hipSuccess;
-  const bool full = !short_launch(P) && !env_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
+  const bool full = !lpt_launch(P) && !env_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
   if (!full) {  // short launch: every launch measured, ordered longest first by the previous one
     P.sched_full = 0;
     if (S.measured) {
