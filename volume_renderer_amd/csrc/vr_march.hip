@@ -724,7 +724,7 @@ __device__ __forceinline__ bool finite3(const f3 &v) {
 #define VR_SCHED1_MIN_EU 1  // a short (scheduled) launch's occupancy cap (A/B; 1: uncapped registers)
 #endif
 constexpr int march_min_eu(int cap, int sched) {
-  return cap <= VR_LDS_CAP ? (sched != 1 ? VR_MARCH_MIN_EU : VR_SCHED1_MIN_EU) : 1;
+  return cap <= VR_LDS_CAP_MARCH ? (sched != 1 ? VR_MARCH_MIN_EU : VR_SCHED1_MIN_EU) : 1;
 }
 #ifndef VR_WG_WAVES
 #define VR_WG_WAVES 4  // waves per workgroup: a 16x16 block stays on one XCD (1 wave: same speed, 2x HBM traffic)
@@ -1121,7 +1121,9 @@ static bool inject_bad_launch() {
   return ev && ev[0] == '1';
 }
 
-template <int MODE, bool AB, bool SH, int CAP>
+// BS: the addressing variants this instantiation holds (1: 32-bit, 2: 64-bit, 3: both) -- the
+// narrow slot differs between them (launch_m), the kernel count does not.
+template <int MODE, bool AB, bool SH, int CAP, int BS = 3>
 static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
   constexpr int K = VR_MARCH_K;
   const dim3 blk(inject_bad_launch() ? 2048 : 64 * VR_WG_WAVES);
@@ -1135,9 +1137,19 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
     hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, 0, s, P);          \
     note_march_kernel(VR_MARCH_FAST, KK, MODE, AB, CNT, SH, BG, CAP, SC);                                 \
   } while (0)
+#define VR_LAUNCH_B(KK, CNT, SC)                                                                           \
+  do {                                                                                                    \
+    if (big) {                                                                                            \
+      if constexpr ((BS & 2) != 0) VR_LAUNCH(KK, CNT, true, SC);                                          \
+      else return hipErrorInvalidValue;                                                                   \
+    } else {                                                                                              \
+      if constexpr ((BS & 1) != 0) VR_LAUNCH(KK, CNT, false, SC);                                         \
+      else return hipErrorInvalidValue;                                                                   \
+    }                                                                                                     \
+  } while (0)
   // paired stereo tiles (SCHED 4): the lit, half-texel-tap, absorption = emission, default-slot,
   // 32-bit launch of K > 1 only (a measurement of what the eyes' staged boxes share)
-  constexpr bool PAIRK = K > 1 && VR_MARCH_FAST && AB && MODE == 1 && SH && CAP == VR_LDS_CAP;
+  constexpr bool PAIRK = K > 1 && VR_MARCH_FAST && AB && MODE == 1 && SH && CAP == VR_LDS_CAP_MARCH && (BS & 1);
   if (P.pair_shift) {
     if constexpr (PAIRK) {
       if (big || sched || (P.steps && !VR_COUNT_K)) return hipErrorInvalidValue;
@@ -1151,8 +1163,7 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   // (the counter variant: instantiated in the K = 1 object only -- or at every K in a VR_COUNT_K build)
   if constexpr (K == 1 || VR_COUNT_K) {
     if (P.steps) {
-      if (big) VR_LAUNCH(K, true, true, 0);
-      else VR_LAUNCH(K, true, false, 0);
+      VR_LAUNCH_B(K, true, 0);
       return hipGetLastError();
     }
   }
@@ -1161,26 +1172,30 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   } else if (sched && !SCH) {  // the exact variant and separate absorption have no scheduled kernels
     return hipErrorInvalidValue;
   } else if (K > 1 && sched && P.sched_full == 1) {  // a full frame, durations measured
-    if (big) VR_LAUNCH(K, false, true, S2);
-    else VR_LAUNCH(K, false, false, S2);
+    VR_LAUNCH_B(K, false, S2);
   } else if (K > 1 && sched && P.sched_full == 2) {  // a full frame in the last measured order
-    if (big) VR_LAUNCH(K, false, true, S3);
-    else VR_LAUNCH(K, false, false, S3);
+    VR_LAUNCH_B(K, false, S3);
   } else if (K > 1 && sched) {  // a short launch (few waves per slot), longest first
-    if (big) VR_LAUNCH(K, false, true, S1);
-    else VR_LAUNCH(K, false, false, S1);
+    VR_LAUNCH_B(K, false, S1);
   } else {
-    if (big) VR_LAUNCH(K, false, true, 0);
-    else VR_LAUNCH(K, false, false, 0);
+    VR_LAUNCH_B(K, false, 0);
   }
+#undef VR_LAUNCH_B
 #undef VR_LAUNCH
   return hipGetLastError();
 }
 
+// The wave slot of a launch: wide (P.wide_slot), else 8 KiB for a 32-bit launch without lookup
+// gradients and 6.5 KiB for the others (vr_stage.h VR_LDS_CAP_MARCH).
 template <int MODE, bool AB, bool SH>
 static hipError_t launch_m(const RenderParams &P, dim3 grid, hipStream_t s, bool big) {
-  return P.wide_slot ? launch_c<MODE, AB, SH, VR_LDS_CAP_WIDE>(P, grid, s, big)
-                     : launch_c<MODE, AB, SH, VR_LDS_CAP>(P, grid, s, big);
+  if (P.wide_slot) return launch_c<MODE, AB, SH, VR_LDS_CAP_WIDE>(P, grid, s, big);
+  // (the exact-arithmetic variant, a parity reference, keeps 6.5 KiB everywhere: 0.5 MiB less code)
+  if constexpr (MODE == 2 || !VR_MARCH_FAST)
+    return launch_c<MODE, AB, SH, VR_LDS_CAP>(P, grid, s, big);
+  else
+    return big ? launch_c<MODE, AB, SH, VR_LDS_CAP, 2>(P, grid, s, big)
+               : launch_c<MODE, AB, SH, VR_LDS_CAP_MARCH, 1>(P, grid, s, big);
 }
 
 // Host entry (launch_march_k1 / _k2 / _k4 / _k8, one per object file): the staged kernel needs a
@@ -1229,7 +1244,7 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
 #else
 // ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation and the matching
 // sort-last slab kernel, for a quick look at their code without compiling every variant.
-template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);
+template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP_MARCH, 0>(const RenderParams P);
 template __global__ void march_kernel<2, 2, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);  // C3
 template __global__ void march_slab_kernel<2, 1, true, VR_LDS_CAP, false>(const RenderParams P);
 #endif  // !VR_ISA_PROBE

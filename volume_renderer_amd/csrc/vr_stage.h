@@ -18,6 +18,14 @@ namespace vr {
 #ifndef VR_LDS_CAP
 #define VR_LDS_CAP 1664        // 6.5 KiB: 26 KiB per workgroup -> 6 workgroups (24 waves) per CU
 #endif
+#ifndef VR_LDS_CAP_MARCH
+// 8 KiB (2040 floats: 5 workgroups per CU, the register-bound occupancy of the march kernel at 96
+// VGPRs, so the larger slot costs no wave) for the 32-bit on-the-fly / emission-only launches --
+// round 5, with every full frame heavy-first: metric frame 27.24-27.57 -> 26.18-26.50 ms on two
+// boxes (r5aw, r5ax), the P = 2 part 15.62 -> 14.87; lookup-gradient (C3 29.4 -> 30.1) and 64-bit
+// (C5 226.1 -> 228.7) launches keep VR_LDS_CAP
+#define VR_LDS_CAP_MARCH 2040
+#endif
 #ifndef VR_LDS_CAP_WIDE
 // 10 KiB: 4 workgroups per CU, for footprints above ~1.5 texels/pixel and every K = 4 launch (round 5:
 // 2560 instead of 3072 floats -- C2 12.23 -> 10.93-10.97 ms, P = 8 part 4.89-4.93 -> 4.82-4.87, r5t;
