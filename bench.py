@@ -93,6 +93,14 @@ def main():
     ap.add_argument("--pipelined-streams", type=int, default=2,
                     help="extra pass (not `value`): the frames issued round-robin on this many HIP streams "
                          "(independent frames of a movie, example3.m); 1 or 0 skips it")
+    ap.add_argument("--movie", type=int, default=30,
+                    help="frames of each movie pass (0: none; world size 1): frame i seen from rotate(start) * "
+                         "rotate(step)^i, as examples/example2.m:53-66 turns the camera before every render -- no "
+                         "frame has an earlier frame of its camera; reported apart from `value`")
+    ap.add_argument("--movie-step", type=float, nargs=3, default=[0.0, 12.0, 0.0],
+                    help="camera turn between movie frames, rotate(alpha, beta, gamma) (example2.m: 0 12 0)")
+    ap.add_argument("--movie-starts", default="125,25,0;30,10,0",
+                    help="';'-separated start cameras of the movie passes, rotate(alpha,beta,gamma) from identity")
     ap.add_argument("--chunk-stats-k", action="store_true",
                     help="diagnostic (a VR_COUNT_K=1 build): also the chunk statistics of the production "
                          "depth lanes (the default counted launch runs at K = 1)")
@@ -124,6 +132,10 @@ def main():
 
     import volume_renderer_amd as vr
     from volume_renderer_amd import mex
+    if os.environ.get("VR_TEST_SWITCHES") == "1" or args.chunk_stats_k:
+        # A/B runs (tools/gpupass.py) select kernel variants through VR_* switches, which the library
+        # reads only with its test switches on (include/vrhip.h vr_set_option)
+        mex.enable_test_switches()
 
     dev = torch.device("cuda", local_rank)
     stream = torch.cuda.current_stream(dev)
@@ -323,6 +335,10 @@ def main():
             sim.append(round(e0.elapsed_time(e1) / 3, 3))
         del sim_out
 
+    movies = None
+    if args.movie > 0 and world == 1:
+        movies = movie_passes(args, mex, h, lights, lut, W, H, stream, sptr, dev, out_local.numel())
+
     samples_all = torch.tensor([my_samples, my_lit], dtype=torch.int64, device=cdev)
     el = torch.tensor([elapsed, pipe_elapsed or 0.0], dtype=torch.float64, device=cdev)
     if world > 1:
@@ -376,21 +392,26 @@ def main():
             "staged_chunks_by_S_32_16_8_4": staged_by_s,
             "probe_runs_leaped_failed": probe_stats,
             "gb_per_s_sample_stream": round(4.0 * total_samples * F / (elapsed / args.steps) / 1e9, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            # achieved / frac: the bytes the samples need (SURVEY 8d's "minimum fetches needed to
+            # reproduce the output" once opacity-0 samples are elided exactly: their shading adds exactly
+            # 0) per launch over the march kernel's mean HIP-event time
+            "roofline": {"bound": "hbm", "achieved": round(fetched / t_kernel_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(fetched / t_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None,
                          "kernel_ms": round(t_kernel_s * 1e3, 3),
                          "kernel": max(timed_kernels, key=timed_kernels.get) if timed_kernels else None,
                          "kernels_timed": timed_kernels,
-                         "bytes_per_launch": bytes_launch,
-                         "algorithmic_bytes": "4 B x samples x F(=%d) + 12 B x pixels" % F,
-                         "note": "SURVEY 8d's definitional sample-stream bytes: every sample charged F fetches, "
-                                 "but opacity-0 samples (60.5 % at the metric config) are leaped or skip their "
-                                 "shading, so frac can exceed 1; the hardware fractions are in `binding` "
-                                 "(DESIGN.md s7)",
-                         "fetched": {"bytes_per_launch": fetched,
-                                     "achieved": round(fetched / t_kernel_s / 1e9, 1),
-                                     "frac": round(fetched / t_kernel_s / 1e9 / HBM_PEAK_GBS, 4),
-                                     "what": "4 B x (samples + shaded samples x (F-1)) + 12 B x pixels"},
+                         "bytes_per_launch": fetched,
+                         "algorithmic_bytes": "4 B x (samples + shaded samples x (F-1)) + 12 B x pixels, F = %d "
+                                              "(every sample its centre fetch; the shaded ones, opacity > 0, also "
+                                              "the gradient / reflection / LUT fetches)" % F,
+                         "sample_stream": {"bytes_per_launch": bytes_launch, "achieved": round(achieved, 1),
+                                           "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                           "what": "SURVEY 8d's definitional 4 B x samples x F + 12 B x pixels: "
+                                                   "every sample charged F fetches, opacity-0 ones (60.5 % at the "
+                                                   "metric config, leaped or unshaded) included, so it can exceed "
+                                                   "1"},
+                         "sample_stream_frac": round(achieved / HBM_PEAK_GBS, 4),
                          "valu": None},
             "cpu_baseline": None,
         }
@@ -406,6 +427,10 @@ def main():
             result["volume_broadcast"] = bcast
         if prod_stats is not None:
             result["chunk_stats_production_k"] = prod_stats
+        if movies is not None:
+            for m in movies:
+                m["median_over_fixed_kernel"] = round(m["median_ms"] / (t_kernel_s * 1e3), 3)
+            result["movie"] = movies
         if sim is not None:
             result["sim_parts_kernel_ms"] = {"parts": args.sim_parts, "per_part": sim, "max": max(sim),
                                              "est_speedup": round(t_kernel_s * 1e3 / max(sim), 2)}
@@ -456,13 +481,58 @@ def main():
         dist.destroy_process_group()
 
 
+def movie_passes(args, mex, h, lights, lut, W, H, stream, sptr, dev, out_floats):
+    """Movies (examples/example2.m:53-66): from each start camera, args.movie frames, each turned by
+    args.movie_step from the previous one, rendered back to back on the bench's stream with HIP events
+    around each frame.  Every frame is a camera the library has not rendered before (the first frame
+    of the metric start aside, which the fixed-camera frames rendered), so its block schedule comes
+    from the occupancy-map prediction, not from a measurement (vr_capi.hip attach_schedule)."""
+    import hashlib
+    step = rotation(*args.movie_step)
+    out = []
+    for spec in args.movie_starts.split(";"):
+        start = [float(v) for v in spec.split(",")]
+        R = rotation(*start)
+        ras, keep, bufs = [], [], []
+        for _ in range(args.movie):
+            ra, kp = mex.render_args(lights, lut, np.float32([1.0, 0.4, 0.6]), np.float32([1, 1, 1]),
+                                     np.uint64([H, W]), np.flip(R, 0).astype(np.float32),
+                                     np.float32([0, 3.0, 6.0]), np.float32(0.9), np.float32([1, 1, 0]))
+            ras.append(ra)
+            keep.append(kp)
+            bufs.append(torch.empty(out_floats, dtype=torch.float32, device=dev))
+            R = R @ step
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in ras]
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for (e0, e1), ra, b in zip(evs, ras, bufs):
+            e0.record(stream)
+            mex.render_device(h, ra, b.data_ptr(), None, 0, sptr)
+            e1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        ms = [a.elapsed_time(b) for a, b in evs]
+        dig = hashlib.sha256()
+        for b in bufs:
+            dig.update(np.ascontiguousarray(b[: 3 * W * H].cpu().numpy()).tobytes())
+        med = float(np.median(ms))
+        out.append({"start": start, "step": list(args.movie_step), "frames": len(ms),
+                    "frame_ms": [round(v, 3) for v in ms], "median_ms": round(med, 3), "max_ms": round(max(ms), 3),
+                    "first_ms": round(ms[0], 3), "max_over_median": round(max(ms) / med, 3),
+                    "wall_ms_per_frame": round(wall / len(ms) * 1e3, 3), "frames_sha256": dig.hexdigest(),
+                    "what": "frame i at rotate(start) * rotate(step)^i, HIP events around each render; no frame "
+                            "repeats a camera (frame 0 of the metric start is the fixed-camera frame)"})
+        del bufs
+    return out
+
+
 def binding_roof(rf, t_kernel_s):
     """The roof nearest to binding the launch: the largest of the fractions that describe hardware
-    use -- the bytes the samples need (`fetched`), the HBM bytes the counters saw (FETCH_SIZE x 2 +
-    WRITE_SIZE, over 8 TB/s) and the VALU issue rate (over its wave64 peak).  The F-weighted sample
-    stream (`frac`) is a definitional figure (it charges F fetches to opacity-0 samples, which the
-    kernel skips; it reads above 1 at C5), so it is not a candidate."""
-    cands = {"fetched": rf["fetched"]["frac"]}
+    use -- the bytes the samples need (`frac`, "fetched"), the HBM bytes the counters saw (FETCH_SIZE x
+    2 + WRITE_SIZE, over 8 TB/s) and the VALU issue rate (over its wave64 peak).  The F-weighted sample
+    stream (`sample_stream_frac`) is a definitional figure (it charges F fetches to opacity-0 samples,
+    which the kernel skips; it reads above 1), so it is not a candidate."""
+    cands = {"fetched": rf["frac"]}
     if rf.get("traffic"):
         cands["hbm_traffic"] = round(rf["traffic"] / t_kernel_s / 1e9 / HBM_PEAK_GBS, 4)
     if rf.get("valu"):

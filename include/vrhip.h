@@ -303,6 +303,13 @@ int64_t vr_hip_errors(char *buf, size_t buflen);
  * bench.py names the kernel it times with it and keys the profiler's counters to it. */
 int vr_last_march_kernel(char *buf, size_t buflen);
 
+/* Process-wide options (round 6; no reference counterpart).  "test_switches" = 1 lets the library
+ * read the kernel-variant and schedule switches the GPU tests and the measurement tools set through
+ * the environment (VR_NO_LDS, VR_DEPTH_LANES, VR_SCHED, ... -- INTEGRATION.md "Runtime switches");
+ * by default (0) they are ignored, so a MATLAB session's environment cannot select them.  Returns
+ * VR_ERR_ARGUMENT for an unknown name. */
+int vr_set_option(const char *name, int64_t value);
+
 /* Library build identification ("libvrhip <version> gfx950 ..."). */
 const char *vr_version(void);
 

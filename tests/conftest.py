@@ -13,6 +13,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _test_switches():
+    """The variant tests select kernels through VR_* environment switches, which the library reads
+    only after vr_set_option("test_switches", 1) (include/vrhip.h; a MATLAB session never sets it)."""
+    try:
+        from volume_renderer_amd import mex
+        mex.enable_test_switches()
+    except (ImportError, OSError):
+        pass  # (no library: the CPU tests that need none)
+    yield
+
+
 def gpu_available() -> bool:
     try:
         import torch

@@ -246,13 +246,15 @@ def test_binding_roof_names_the_largest_hardware_fraction():
     import sys
     sys.path.insert(0, ROOT)
     import bench
-    rf = {"frac": 1.07, "fetched": {"frac": 0.46}, "traffic": 1.0e12, "valu": {"frac": 0.62}}
+    # (round 6: frac is the needed-bytes fraction; the F-weighted one is sample_stream_frac)
+    rf = {"frac": 0.46, "sample_stream_frac": 1.07, "traffic": 1.0e12, "valu": {"frac": 0.62}}
     b = bench.binding_roof(rf, 0.265)  # 1 TB in 265 ms = 3.77 TB/s = 0.47 of 8 TB/s
     assert b["roof"] == "valu" and b["frac"] == 0.62
     assert abs(b["candidates"]["hbm_traffic"] - 1.0e12 / 0.265 / 8e12) < 1e-3
-    b = bench.binding_roof({"frac": 0.9, "fetched": {"frac": 0.23}, "traffic": 1.05e11, "valu": None}, 0.017)
+    b = bench.binding_roof({"frac": 0.23, "sample_stream_frac": 0.9, "traffic": 1.05e11, "valu": None}, 0.017)
     assert b["roof"] == "hbm_traffic" and set(b["candidates"]) == {"fetched", "hbm_traffic"}
-    assert bench.binding_roof({"frac": 0.9, "fetched": {"frac": 0.4}, "traffic": None, "valu": None}, 0.03)["roof"] == "fetched"
+    assert bench.binding_roof({"frac": 0.4, "sample_stream_frac": 0.9, "traffic": None, "valu": None},
+                              0.03)["roof"] == "fetched"
 
 
 def test_cpu_share_is_positive():

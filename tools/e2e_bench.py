@@ -40,6 +40,7 @@ def main():
     torch.cuda.set_device(0)
     import volume_renderer_amd as vr
     from volume_renderer_amd import mex
+    mex.enable_test_switches()  # (the VR_* variant switches this tool sets)
     from bench import rotation
 
     n, W, H = args.n, args.width, args.height

@@ -62,7 +62,7 @@ def step_ab(out, rest, idx, bench_args):
     extra = shlex.split(bench_args)
     for r in range(int(rounds)):
         for name, env in specs:
-            e = dict(os.environ)
+            e = dict(os.environ, VR_TEST_SWITCHES="1")  # (bench.py: the library reads the VR_* switches)
             e.update(env)
             res = os.path.join(out, f"ab{idx}_{name}_{r}.json")
             cmd = [PY, "bench.py", "--steps", "20", "--warmup", "4", "--no-cpu-baseline", "--pipelined-streams", "0"]

@@ -44,6 +44,7 @@ def render(sc):
     """Product render of the scene through the 'render' mex command; returns (img, device tensor)."""
     import volume_renderer_amd as vr
     from volume_renderer_amd import mex
+    mex.enable_test_switches()  # (the VR_* variant switches this tool sets)
     import test_full_size as T
     t = T.device_structure(sc["n"]) if sc["gen"] == "structure" else T.device_shell(sc["n"])
     dims = (sc["n"],) * 3

@@ -54,6 +54,7 @@ def main():
             dist.init_process_group(args.backend)
     import volume_renderer_amd as vr
     from volume_renderer_amd import mex, parallel
+    mex.enable_test_switches()  # (the VR_* variant switches this tool sets)
     from bench import rotation
 
     n, W, H = args.volume, args.width, args.height

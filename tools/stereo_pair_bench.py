@@ -35,6 +35,7 @@ import oracle as O  # noqa: E402
 
 
 def main():
+    mex.enable_test_switches()  # (the VR_* variant switches this tool sets)
     out_path = sys.argv[1] if len(sys.argv) > 1 else None
     n, W, H = 1024, 1920, 1080
     f, dist, xoff = 4.5, 6.0, 0.06

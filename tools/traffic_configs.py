@@ -72,7 +72,8 @@ def attach(line, e, src):
         rf["valu"] = {"insts_per_launch": vi, "achieved": round(vi / t / 1e9, 2),
                       "peak": round(VALU_ISSUE_PER_S / 1e9, 1), "unit": "G wave64-instr/s",
                       "frac": round(vi / t / VALU_ISSUE_PER_S, 4)}
-    cands = {"fetched": rf["fetched"]["frac"], "hbm_traffic": round(rf["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4)}
+    fr = rf["fetched"]["frac"] if "fetched" in rf else rf["frac"]  # (round 6: frac is the fetched fraction)
+    cands = {"fetched": fr, "hbm_traffic": round(rf["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4)}
     if vi:
         cands["valu"] = rf["valu"]["frac"]
     name = max(cands, key=cands.get)

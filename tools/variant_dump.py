@@ -10,6 +10,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
 sys.path.append(os.path.join(os.path.dirname(__file__), ".."))
 import oracle as O  # noqa: E402  (checker only: builds the synthetic shell volume)
 import volume_renderer_amd as vr  # noqa: E402
+vr.mex.enable_test_switches()  # (the VR_* variant switches this tool sets)
 from test_gpu_parity import ex1_renderer  # noqa: E402
 
 VARIANTS = [("default", {}), ("plain", {"VR_NO_LDS": "1"}), ("noskip", {"VR_NO_EMPTY_SKIP": "1"}),

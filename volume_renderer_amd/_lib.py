@@ -102,6 +102,7 @@ SIGNATURES = [
     ("vr_last_error", c_char_p, []),
     ("vr_hip_errors", c_int64, [c_char_p, c_size_t]),
     ("vr_last_march_kernel", c_int, [c_char_p, c_size_t]),
+    ("vr_set_option", c_int, [c_char_p, c_int64]),
     ("vr_version", c_char_p, []),
 ]
 

@@ -75,7 +75,10 @@ hipError_t launch_iota(uint32_t *order, uint32_t n, hipStream_t s);
 hipError_t launch_pad(const float *src, float *dst, int32_t nx, int32_t ny, int32_t nz, hipStream_t s);
 hipError_t launch_stats(const float *src, uint64_t n, BufStats *st, hipStream_t s);
 hipError_t launch_zpair(const float *src, float *dst, uint32_t n, uint32_t pxy, hipStream_t s);
-hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, hipStream_t s);
+hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, float inv_scale,
+                            hipStream_t s);
+hipError_t launch_predict_cost(const RenderParams &P, uint32_t nb_view, uint32_t nbx, int32_t tw, int32_t th,
+                               int32_t m, float dens, float xthr, uint32_t *cost, hipStream_t s);
 uint64_t interleave3_entries(uint32_t px, uint32_t py, uint32_t pz);
 hipError_t launch_interleave3(const float *a, const float *b, const float *c, float *out, uint32_t px,
                               uint32_t py, uint32_t pz, hipStream_t s);
@@ -109,9 +112,6 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 // 26.37-26.64, / 4 26.80-27.17, / 2 28.27-28.82; r5ae, r5af); C3 28.83 -> 28.62, C2 and C5 unchanged
 #define VR_SCHED_TAIL_PCT 0
 #endif
-#ifndef VR_SCHED_SHIFT
-#define VR_SCHED_SHIFT 0.0  // full frames: heavy blocks moved ahead by this many block rows x duration / longest
-#endif
 #ifndef VR_SCHED_REMEASURE
 #define VR_SCHED_REMEASURE 16  // full frames: block durations re-measured every this many launches
 #endif
@@ -126,7 +126,11 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 #define VR_SCHED_ROUNDS 6.0      // longest-first schedule below this many K = 1 waves per wave slot
 #endif
 
+namespace {
+std::atomic<int> g_test_switches{0};  // vr_set_option("test_switches"), see test_env below
+}
 namespace vr {
+bool test_switches_on() { return g_test_switches.load() != 0; }
 std::string &last_march_kernel() {
   static std::string name;
   return name;
@@ -258,9 +262,12 @@ struct vr_context {
     // full frames: the measured durations copied to the host (asynchronously, after the launch) to
     // decide whether the heaviest block would form a tail
     uint32_t *h_cost = nullptr;
-    uint32_t *h_order = nullptr;  // pinned: a host-computed order (VR_SCHED_SHIFT / VR_SCHED_ROWS)
     hipEvent_t copied = nullptr;
+    uint32_t renders = 0;  // full frames: renders of this frame key so far
     bool copy_pending = false, decided = false, tail = false;
+    // round 6: the frame (camera, volume upload, opacity parameters, frame_key) the durations were
+    // measured on, and the one the order in d_order was predicted for (0: none)
+    uint64_t key = 0, pred_key = 0;
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -369,6 +376,20 @@ bool diag_flag(const char *name) {
   const char *ev = diag_env(name);
   return ev && ev[0] == '1';
 }
+// Test switches (round 6, INTEGRATION.md "Runtime switches"): the kernel-variant and schedule
+// switches the GPU tests and the measurement tools set through the environment are read only after
+// vr_set_option("test_switches", 1) (tests/conftest.py, bench.py diagnostics, tools/) or in a DIAG=1
+// build, so that a MATLAB session's environment never selects them.  The production switches
+// (VR_EXACT_SHADE, VR_ALWAYS_REUPLOAD, VR_GROUP_PEER, the upload ring's) are read always.
+const char *test_env(const char *name) { return (VR_DIAG || g_test_switches.load()) ? std::getenv(name) : nullptr; }
+bool test_flag(const char *name) {
+  const char *ev = test_env(name);
+  return ev && ev[0] == '1';
+}
+bool test_flag_off(const char *name) {
+  const char *ev = test_env(name);
+  return ev && ev[0] == '0';
+}
 
 // syncVolume (kernel.cu:659-672): unbind the texture, drop the old array, upload the volume into a
 // device buffer and bind it.  The handle's previous buffer of the slot is rewritten in place when
@@ -411,7 +432,7 @@ void build_zpair(DevBuf *b, hipStream_t s) {
 #endif
 void build_occupancy(DevBuf *b, hipStream_t s) {
   const uint64_t px = b->dims[0] + 2, py = b->dims[1] + 2, pz = b->dims[2] + 2;
-  const bool want = px * py * pz >= VR_OCC_MIN_VOXELS && px < (1ull << 31) && !env_flag("VR_NO_PROBE");
+  const bool want = px * py * pz >= VR_OCC_MIN_VOXELS && px < (1ull << 31) && !test_flag("VR_NO_PROBE");
   constexpr uint64_t E = 1u << VR_OCC_LOG;  // brick edge
   const uint64_t bytes = want ? ((px + E - 1) / E) * ((py + E - 1) / E) * ((pz + E - 1) / E) : 0;
   if (!want || b->occ_bytes != bytes) {
@@ -424,7 +445,10 @@ void build_occupancy(DevBuf *b, hipStream_t s) {
     VR_HIP(vr_host::pooled_alloc(reinterpret_cast<void **>(&b->occ), bytes, b->device));
     b->occ_bytes = bytes;
   }
-  VR_HIP(vr::launch_occupancy(b->ptr, (uint32_t)px, (uint32_t)py, (uint32_t)pz, b->occ, s));
+  // (the bytes also carry each brick's mean |voxel| for the schedule predictor, in 1/255 of the largest)
+  const float inv = (!b->nonfinite && b->maxabs > 0.f) ? 255.f / b->maxabs : 0.f;
+  VR_HIP(vr::launch_occupancy(b->ptr, (uint32_t)px, (uint32_t)py, (uint32_t)pz, b->occ, std::isfinite(inv) ? inv : 0.f,
+                              s));
   VR_HIP(hipStreamSynchronize(s));
 }
 
@@ -455,7 +479,7 @@ void sync_volume(vr_context *h, int tex, int slot) {
     b->nonfinite = st.nonfinite != 0;
     b->maxabs = st.maxabs;
     if (tex == T_LIGHT) build_zpair(b.get(), U.stream);
-    else build_occupancy(b.get(), U.stream);
+    else if (tex <= T_RE) build_occupancy(b.get(), U.stream);  // (only these can be bound as emission)
   } else {
     build_occupancy(b.get(), nullptr);  // (an empty volume: drops a previous map)
   }
@@ -607,7 +631,7 @@ vr::DevTex dev_tex(const BufPtr &b) {
     t.fnz = (float)t.nz;
     t.one = (t.nx == 1 && t.ny == 1 && t.nz == 1);
     const uint64_t padded = (b->dims[0] + 2) * (b->dims[1] + 2) * (b->dims[2] + 2);
-    t.small = padded < (1ull << 22) && !env_flag("VR_NO_SMALL_LUT");
+    t.small = padded < (1ull << 22) && !test_flag("VR_NO_SMALL_LUT");
     t.fpx4 = 4.f * (float)t.px;
     t.fpxy4 = 4.f * (float)t.pxy;
     t.fbase4 = 4.f * (float)(t.pxy + t.px + 1);
@@ -640,7 +664,7 @@ bool tame(const BufPtr &b) { return !b || !b->ptr || (!b->nonfinite && b->maxabs
 // 8-bit weight quantization (measured: tests/test_gpu_parity.py::test_half_texel_taps).
 // VR_EXACT_TAPS=1 turns it off.
 int32_t half_texel_taps(const vr::RenderParams &P, int mode, float fnz) {
-  if (mode != 1 || env_flag("VR_EXACT_TAPS")) return 0;
+  if (mode != 1 || test_flag("VR_EXACT_TAPS")) return 0;
   const float n[3] = {P.em.fnx, P.em.fny, fnz};
   for (int i = 0; i < 3; ++i) {
     int e = 0;
@@ -677,6 +701,11 @@ void drift_bound(Frame &F, const float *eye2) {
   for (int i = 0; i < 3; ++i) {
     const float n = i == 0 ? P.em.fnx : (i == 1 ? P.em.fny : P.em.fnz);
     F.drift1[i] = 2.0 * pmax * 1.2e-7 * (double)P.bscale[i] * (double)n;
+    // the empty-space probe's box: the centre taps (the cell of floor(c n - 1/2)) with the staging
+    // margin of 1/16 texel, plus the drift of up to VR_PROBE_MAX sequential additions.  Set here, with
+    // the drift, so that every launch path gets it -- the fused multi-view march included (ADVICE r5:
+    // it copied F.P before set_chunk_halo and probed with a zero margin)
+    F.P.probe_off[i] = (float)(0.0625 + (double)VR_PROBE_MAX * F.drift1[i]);
   }
 }
 
@@ -795,7 +824,7 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
     const double rmax = (rb && rb->ptr) ? rb->maxabs : 0.0, lutmax = (lb && lb->ptr) ? lb->maxabs : 0.0;
     ok = ok && (double)std::fabs(P.fr) * rmax * lutmax * lmax * bound * (double)(g_tex.lights.size() + 1) < 1e36;
     P.skip_empty = ok ? 1 : 0;
-    if (const char *ev = std::getenv("VR_NO_EMPTY_SKIP"))  // A/B switch for measurements
+    if (const char *ev = test_env("VR_NO_EMPTY_SKIP"))  // A/B switch for measurements
       if (ev[0] == '1') P.skip_empty = 0;
   }
   // Per-sample range tests the upload statistics decide for the whole launch (vr_sampling.h): every
@@ -821,7 +850,12 @@ int build_frame(vr_context *h, const vr_render_args *a, Frame &F, uint64_t depth
     P.re_mask = P.re_is_em ? 0xffffffffu : 0u;
   }
   F.big = is_big(P.em) || is_big(P.ab) || is_big(P.re) || is_big(P.gem) || is_big(P.gx) || is_big(P.gy) ||
-          is_big(P.gz) || env_flag("VR_FORCE_BIG");  // test switch: the 64-bit path on small volumes
+          is_big(P.gz) || test_flag("VR_FORCE_BIG");  // test switch: the 64-bit path on small volumes
+  // the lookup gradient's bricked copy has 8 ceil(px/2) ceil(py/2) ceil(pz/2) entries, more than the
+  // padded voxels: just under 2^32 voxels its 32-bit entry index would wrap (e.g. 1623^3)
+  if (F.mode == 2 && P.gx.p &&
+      vr::interleave3_entries(P.gx.px, P.gx.pxy / P.gx.px, (uint32_t)P.gx.nz + 2u) > 0xFFFFFFFFull)
+    F.big = true;
   if (is_big(P.lut)) return fail(VR_ERR_UNSUPPORTED, "illumination volume larger than 2^32 voxels");
   bool finite = std::isfinite(P.tstep) && P.tstep > 0.f;
   for (int i = 0; i < 3; ++i) finite = finite && std::isfinite(P.bmin[i]) && std::isfinite(P.bscale[i]);
@@ -896,9 +930,6 @@ int chunk_samples(int K) { return K >= 2 ? 16 * K : 32; }
 void set_chunk_halo(Frame &F, int K) {
   for (int i = 0; i < 3; ++i) {
     F.P.tap_off[i] += (float)(chunk_samples(K) * F.drift1[i]);
-    // the empty-space probe's box: the centre taps (the cell of floor(c n - 1/2)) with the staging
-    // margin of 1/16 texel, plus the drift of up to VR_PROBE_MAX sequential additions
-    F.P.probe_off[i] = (float)(0.0625 + (double)VR_PROBE_MAX * F.drift1[i]);
   }
 }
 
@@ -914,7 +945,6 @@ void free_schedules(vr_context *h) {
     if (kv.second.d_cost) (void)hipFree(kv.second.d_cost);
     if (kv.second.d_order) (void)hipFree(kv.second.d_order);
     if (kv.second.h_cost) (void)hipHostFree(kv.second.h_cost);
-    if (kv.second.h_order) (void)hipHostFree(kv.second.h_order);
     if (kv.second.copied) (void)hipEventDestroy(kv.second.copied);
   }
   h->sched.clear();
@@ -954,7 +984,7 @@ int device_wave_slots() {
 #endif
 
 int depth_lanes(const vr::RenderParams &P) {
-  if (const char *ev = std::getenv("VR_DEPTH_LANES")) {
+  if (const char *ev = test_env("VR_DEPTH_LANES")) {
     const int k = std::atoi(ev);
     if (k == 1 || k == 2 || k == 4 || (k == 8 && VR_WITH_K8)) return k;
   }
@@ -986,7 +1016,7 @@ void set_tau_and_slot(vr::RenderParams &P, const vr_render_args *a, double vw) {
   // measured the opposite at K = 4 (20.7 vs 19.5 ms at C2), when every empty chunk staged its box.
   const int K = P.steps ? 1 : depth_lanes(P);
   P.wide_slot = (tau > 1.5 || (K >= 4 && !P.lookup)) ? 1 : 0;  // (lookup frames: r5y above)
-  if (const char *ev = std::getenv("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
+  if (const char *ev = test_env("VR_WIDE_SLOT")) P.wide_slot = std::atoi(ev) ? 1 : 0;
 }
 
 // The render command proper (render.cpp:134-259 minus the mxArray plumbing).
@@ -1024,13 +1054,82 @@ bool lpt_launch(const vr::RenderParams &P) {
 bool want_schedule(const vr::RenderParams &P) {
   // fused stereo (two views in one launch, vr_render_stereo) is scheduled over both views' blocks;
   // not the paired-tile measurement (VR_STEREO_PAIR), nor the multi-view channel kernel
-  if (P.views > 2 || (P.views == 2 && env_flag("VR_STEREO_PAIR")) || env_flag_off("VR_SCHED")) return false;
-  return env_flag("VR_SCHED") || short_launch(P) || !env_flag_off("VR_SCHED_FULL");
+  if (P.views > 2 || (P.views == 2 && test_flag("VR_STEREO_PAIR")) || test_flag_off("VR_SCHED")) return false;
+  return test_flag("VR_SCHED") || short_launch(P) || !test_flag_off("VR_SCHED_FULL");
 }
 
 // launch_order's tail argument: (tail_pct << 32) | resident workgroups; tail_pct 0 = heavy-first.
 uint64_t wg_tail_arg(uint32_t tail_pct) {
   return (uint64_t)tail_pct << 32 | (uint64_t)(device_wave_slots() / 16 * 6);
+}
+
+// What a tile block's cost depends on beyond the launch shape (round 6): the camera (eyes, axes,
+// focal length), the sampling (box, step), the opacity parameters and the volume -- the emission
+// buffer and the upload its occupancy map was built from.  A schedule measured or predicted under
+// another key is stale (a movie turns the camera every frame, examples/example2.m:53-66).
+uint64_t frame_key(const vr::RenderParams &P) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a
+  auto mix = [&h](const void *p, size_t n) {
+    const unsigned char *c = static_cast<const unsigned char *>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  mix(P.eye, sizeof P.eye);
+  mix(P.eye2, sizeof P.eye2);
+  mix(P.nx_, sizeof P.nx_);
+  mix(P.ydir, sizeof P.ydir);
+  mix(P.zdir, sizeof P.zdir);
+  mix(&P.focal, sizeof P.focal);
+  mix(P.bmin, sizeof P.bmin);
+  mix(&P.tstep, sizeof P.tstep);
+  mix(&P.thr, sizeof P.thr);
+  mix(&P.fa, sizeof P.fa);
+  mix(&P.fe, sizeof P.fe);
+  mix(&P.em.p, sizeof P.em.p);
+  mix(&P.occ, sizeof P.occ);
+  const BufPtr &eb = g_tex.bind[g_tex.idx_em];
+  const uint64_t ver = (eb && eb->ptr == P.em.p) ? eb->version : 0;
+  mix(&ver, sizeof ver);
+  return h | 1u;  // never 0
+}
+
+#ifndef VR_PRED_STEP_TEXELS
+#define VR_PRED_STEP_TEXELS 8.0  // the predictor's step along a ray, in texels (one occupancy brick)
+#endif
+// The predicted block costs of this launch into cost[] (vr_kernels.hip predict_cost_kernel): from
+// the emission texture's occupancy map, the early exit modelled with the absorption (= emission,
+// the scheduled launches' aliasing) bricks' mean densities.
+hipError_t predict_costs(const vr::RenderParams &P, int K, uint32_t nb_view, uint32_t *cost, hipStream_t stream) {
+  const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2)), TH = K <= 2 ? 8 : 4;  // vr_march.hip TileShape
+  const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
+  const BufPtr &eb = g_tex.bind[g_tex.idx_em];
+  double dens = 0.0;
+  if (eb && !eb->nonfinite && P.fa > 0.f && std::isfinite(P.fa))
+    dens = (double)P.fa * (double)eb->maxabs / 255.0 * (double)P.tstep;
+  const double xthr = P.thr < 1.f ? -std::log1p(-(double)std::max(P.thr, 0.f)) : 1e30;
+  // samples per predictor step: ~VR_PRED_STEP_TEXELS texels along the axis a sample advances most on
+  double tpa = 0.0;  // texels per world unit, largest axis
+  for (int i = 0; i < 3; ++i) {
+    const float n = i == 0 ? P.em.fnx : (i == 1 ? P.em.fny : P.em.fnz);
+    tpa = std::max(tpa, (double)P.bscale[i] * (double)n);
+  }
+  const double per = (double)P.tstep * tpa;  // texels per sample at most
+  const int m = (int)std::max(1.0, std::min(4096.0, std::floor(VR_PRED_STEP_TEXELS / std::max(per, 1e-9))));
+  const hipError_t rc = vr::launch_predict_cost(P, nb_view, nbx, TW, TH, m, (float)dens, (float)std::min(xthr, 1e30),
+                                                cost, stream);
+  // VR_SCHED_PRED_DUMP=file (DIAG build): append the predicted costs as tools/sched_dump.py's records
+  if (const char *dump = rc == hipSuccess ? diag_env("VR_SCHED_PRED_DUMP") : nullptr) {
+    const uint32_t nb = nb_view * (uint32_t)std::max(1, (int)P.views);
+    std::vector<uint32_t> c(nb);
+    VR_HIP(hipMemcpyAsync(c.data(), cost, (size_t)nb * 4, hipMemcpyDeviceToHost, stream));
+    VR_HIP(hipStreamSynchronize(stream));
+    const uint32_t hdr[4] = {(uint32_t)K, (uint32_t)P.part, (uint32_t)P.num_parts, nb};
+    if (FILE *f = std::fopen(dump, "ab")) {
+      std::fwrite(hdr, 4, 4, f);
+      std::fwrite(c.data(), 4, c.size(), f);
+      std::fclose(f);
+    }
+  }
+  return rc;
 }
 
 // Attach the schedule of this launch shape (`extra` tells launches of one shape apart, e.g. the
@@ -1041,7 +1140,8 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   static const blocks_fn bfns[4] = {vr::fast::march_blocks_k1, vr::fast::march_blocks_k2, vr::fast::march_blocks_k4,
                                     VR_K8(vr::fast::march_blocks_k8, vr::fast::march_blocks_k4)};
   const int ki = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
-  const uint32_t nb = bfns[ki](P) * (uint32_t)std::max(1, (int)P.views);  // (fused stereo: both views' blocks)
+  const uint32_t nb_view = bfns[ki](P);
+  const uint32_t nb = nb_view * (uint32_t)std::max(1, (int)P.views);  // (fused stereo: both views' blocks)
   // keyed by stream too: the order buffer of one stream is never rewritten under another's launch
   char key[300];
   std::snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%d/%d/%d/%d/%u/%p/%s", K, P.width, P.height, P.part, P.num_parts,
@@ -1061,46 +1161,60 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
   }
   if (!(S.d_cost && S.blocks == nb)) return hipSuccess;
   hipError_t rc = hipSuccess;
-  const bool full = !lpt_launch(P) && !env_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
+  const bool full = !lpt_launch(P) && !test_flag("VR_SCHED");  // VR_SCHED=1: longest-first everywhere
+  // Round 6: block costs predicted from the occupancy map (predict_costs) wherever no measurement of
+  // this very frame exists -- every full frame, and a short launch whose camera or volume changed.
+  // VR_SCHED_MEASURED=1 (DIAG build, A/B): the round-5 schedules from measured durations only.
+  const uint64_t fkey = frame_key(P);
+  const bool predict = P.occ && P.occ_bx && !diag_flag("VR_SCHED_MEASURED");
   if (!full) {  // short launch: every launch measured, ordered longest first by the previous one
     P.sched_full = 0;
-    if (S.measured) {
+    if (S.measured && S.key == fkey) {
       rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, 0u, 0u);
-    } else {  // first launch of this shape: row-major order, durations recorded
+    } else if (predict) {  // no measurement of this frame: longest first by the predicted costs
+      rc = predict_costs(P, K, nb_view, S.d_cost, stream);
+      if (rc == hipSuccess) rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, 0u, 0u);
+    } else {  // first launch of this frame without a map: row-major order, durations recorded
       rc = vr::launch_iota(S.d_order, nb, stream);
-      S.measured = true;
     }
+    S.measured = true;  // (this launch records its durations)
+    S.key = fkey;
+    S.pred_key = 0;
   } else {
-    // full frame: the block durations are measured on the first launch of the shape and every
-    // VR_SCHED_REMEASURE-th after (a scheduled full-frame kernel costs ~5 %, so it runs only when
-    // needed) and copied to the host after the launch; once they arrive, the host decides whether
-    // the heaviest block would form a tail (>= VR_SCHED_TAIL_PCT % of the packed frame: the sum of
-    // durations over the resident workgroups).  Tail: the frames follow the heavy-first order
-    // (order_heavy_kernel) without timing hooks; no tail: no schedule at all (row-major).
+    // Full frame.  Round 6: the first render of a frame (camera, volume: frame_key) follows the
+    // heavy-first order (order_heavy_kernel) of the block costs predicted from the occupancy map,
+    // untimed -- a movie turns the camera every frame (examples/example2.m:53-66), so most of its
+    // frames are first renders; the second render of the same frame runs timed in that order, and
+    // once its durations have reached the host every later render follows the heavy-first order of
+    // the measured durations (re-measured every VR_SCHED_REMEASURE-th render; a timed full-frame
+    // kernel costs ~5 %).  Without a map (small volumes) the first render is the timed row-major
+    // launch.  Whether the heaviest measured block would form a tail (>= VR_SCHED_TAIL_PCT % of the
+    // packed frame: the sum of durations over the resident workgroups) decides between the
+    // heavy-first order and none (round 5: VR_SCHED_TAIL_PCT 0, always heavy-first).
+    if (S.key != fkey) {  // another camera or volume: what was measured does not describe this frame
+      if (S.copy_pending) {
+        (void)hipEventSynchronize(S.copied);
+        S.copy_pending = false;
+      }
+      S.measured = S.decided = S.tail = S.order_stale = false;
+      S.frames = S.renders = 0;
+      S.key = fkey;
+    }
+    ++S.renders;
     uint32_t every = VR_SCHED_REMEASURE;
-    if (const char *ev = std::getenv("VR_SCHED_REMEASURE")) every = (uint32_t)std::max(1, std::atoi(ev));
+    if (const char *ev = test_env("VR_SCHED_REMEASURE")) every = (uint32_t)std::max(1, std::atoi(ev));
     uint32_t heavy_div = VR_SCHED_HEAVY_DIV;
     if (const char *ev = diag_env("VR_SCHED_HEAVY_DIV")) heavy_div = (uint32_t)std::max(1, std::atoi(ev));
     uint32_t tail_pct = VR_SCHED_TAIL_PCT;
-    if (const char *ev = std::getenv("VR_SCHED_TAIL_PCT")) tail_pct = (uint32_t)std::max(0, std::atoi(ev));
+    if (const char *ev = test_env("VR_SCHED_TAIL_PCT")) tail_pct = (uint32_t)std::max(0, std::atoi(ev));
     if (!S.h_cost) {
       hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&S.h_cost), nb * sizeof(uint32_t));
-      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&S.h_order), nb * sizeof(uint32_t));
       if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
       if (e != hipSuccess) {
         vr_host::consume(e, "hipHostMalloc / hipEventCreate (full-frame schedule; none used)");
         return hipSuccess;  // no schedule
       }
     }
-    // VR_SCHED_ROWS=1 (A/B): tile rows of workgroups in the order of their heaviest block, each row
-    // in its own order -- the heavy band early, row-major neighbours still together
-    const bool rows = diag_flag("VR_SCHED_ROWS");
-    // VR_SCHED_SHIFT=r: row-major order with each block moved ahead by r block rows times its
-    // duration over the longest block's -- the heavy blocks start early enough to finish with the
-    // frame, row-major neighbours stay together (L2), and the frame ends on light blocks
-    double shift = VR_SCHED_SHIFT;
-    if (const char *ev = diag_env("VR_SCHED_SHIFT")) shift = std::max(0.0, std::atof(ev));
-    if (rows) shift = 0.0;
     if (S.copy_pending && vr_host::query_done(S.copied, "hipEventQuery (schedule durations)")) {  // arrived
       S.copy_pending = false;
       uint64_t sum = 0;
@@ -1110,63 +1224,49 @@ hipError_t attach_schedule(vr_context *h, vr::RenderParams &P, Frame &F, int K, 
         mx = std::max(mx, S.h_cost[i]);
       }
       const uint64_t wg_slots = std::max<uint64_t>(1, (uint64_t)(device_wave_slots() / 16 * 6));
-      S.tail = rows || shift > 0.0 || (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
+      S.tail = (uint64_t)mx * 100u >= (sum / wg_slots) * tail_pct;
       S.decided = true;
       S.order_stale = true;
-      // workgroup wg is tile block (wg % nbx, wg / nbx) (vr_march.hip march_kernel)
-      const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
-      const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
-      if (shift > 0.0 && mx > 0) {
-        std::vector<std::pair<double, uint32_t>> key(nb);
-        const double per = shift * (double)nbx / (double)mx;
-        for (uint32_t i = 0; i < nb; ++i) key[i] = {(double)i - per * (double)S.h_cost[i], i};
-        std::stable_sort(key.begin(), key.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-        for (uint32_t i = 0; i < nb; ++i) S.h_order[i] = key[i].second;
-        // stream-ordered before every later launch; h_order is rewritten only after the next
-        // measurement's copy (later on this stream) has completed
-        VR_HIP(hipMemcpyAsync(S.d_order, S.h_order, nb * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-        S.order_stale = false;
-      }
-      if (rows) {
-        const uint32_t nr = (nb + nbx - 1) / nbx;
-        std::vector<std::pair<uint32_t, uint32_t>> rk(nr);
-        for (uint32_t r = 0; r < nr; ++r) {
-          uint32_t m = 0;
-          for (uint32_t i = r * nbx; i < std::min(nb, (r + 1) * nbx); ++i) m = std::max(m, S.h_cost[i]);
-          rk[r] = {m, r};
-        }
-        std::stable_sort(rk.begin(), rk.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
-        std::vector<uint32_t> ord;
-        ord.reserve(nb);
-        for (const auto &x : rk)
-          for (uint32_t i = x.second * nbx; i < std::min(nb, (x.second + 1) * nbx); ++i) ord.push_back(i);
-        // (ordered on the launch stream, from the pinned order buffer, as the VR_SCHED_SHIFT order)
-        std::copy(ord.begin(), ord.end(), S.h_order);
-        VR_HIP(hipMemcpyAsync(S.d_order, S.h_order, nb * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-        S.order_stale = false;
-      }
     }
-    bool measure = !S.measured;
-    if (S.measured && !S.copy_pending && ++S.frames >= every) measure = true;
-    if (measure) {
-      S.frames = 0;
-      if (S.decided && S.tail) {  // measured in the heavy-first order the frames use
-        if (S.order_stale) rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
+    if (predict && !S.decided) {  // nothing measured of this frame (yet): the predicted order
+      if (S.pred_key != fkey) {
+        rc = predict_costs(P, K, nb_view, S.d_cost, stream);
+        if (rc == hipSuccess) rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
+        S.pred_key = rc == hipSuccess ? fkey : 0;
+      }
+      // (VR_SCHED_PREDICT_ONLY=1, DIAG build: never measured -- the predictor's own order, A/B)
+      if (S.renders >= 2 && !S.measured && !diag_flag("VR_SCHED_PREDICT_ONLY")) {  // a repeated frame: measured once
+        S.measured = true;
+        S.frames = 0;
+        P.sched_full = 1;
+        F.sched_copy = &S;
       } else {
-        rc = vr::launch_iota(S.d_order, nb, stream);
+        P.sched_full = 2;
       }
-      S.order_stale = false;
-      S.measured = true;
-      P.sched_full = 1;  // timed; the durations are copied back after the launch
-      F.sched_copy = &S;
-    } else if (S.decided && S.tail) {
-      if (S.order_stale) {
-        rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
-        S.order_stale = false;
-      }
-      P.sched_full = 2;  // the heavy-first order, untimed
     } else {
-      return hipSuccess;  // no tail (or not known yet): the unscheduled row-major launch
+      S.pred_key = 0;  // (d_cost holds durations from here on)
+      bool measure = !S.measured;
+      if (S.measured && !S.copy_pending && ++S.frames >= every) measure = true;
+      if (measure) {
+        S.frames = 0;
+        if (S.decided && S.tail) {  // measured in the heavy-first order the frames use
+          if (S.order_stale) rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
+        } else {
+          rc = vr::launch_iota(S.d_order, nb, stream);
+        }
+        S.order_stale = false;
+        S.measured = true;
+        P.sched_full = 1;  // timed; the durations are copied back after the launch
+        F.sched_copy = &S;
+      } else if (S.decided && S.tail) {
+        if (S.order_stale) {
+          rc = vr::launch_order(S.d_cost, nb, S.d_order, stream, heavy_div, wg_tail_arg(0));
+          S.order_stale = false;
+        }
+        P.sched_full = 2;  // the heavy-first order, untimed
+      } else {
+        return hipSuccess;  // no tail (or not known yet): the unscheduled row-major launch
+      }
     }
   }
   if (rc != hipSuccess) return rc;
@@ -1229,11 +1329,11 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   // shading arithmetic: hardware rsq / exp2 by default; VR_EXACT_SHADE=1 selects
   // the oracle's correctly rounded op sequence (bit-identical to oracle/vr_oracle.c up to acosf)
   P.fast_shade = env_flag("VR_EXACT_SHADE") ? 0 : 1;
-  if (const char *ev = std::getenv("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
+  if (const char *ev = test_env("VR_TILE_MODE")) P.tile_mode = std::atoi(ev) ? 1 : 0;  // A/B switch
   // XCD runs of 16 blocks for lookup-gradient frames (their gathers of the gradient copy are the
   // launch's HBM traffic: C3 36.4 -> 35.7 ms, round 4); the compute-gradient march is indifferent
   P.xcd_run = F.mode == 2 ? 32 : VR_XCD_RUN;  // (round 5: 32 / 16 -> 31.24-31.26 / 31.43-31.67 ms, r5p)
-  if (const char *ev = std::getenv("VR_XCD_RUN")) P.xcd_run = std::max(0, std::atoi(ev));  // A/B switch
+  if (const char *ev = test_env("VR_XCD_RUN")) P.xcd_run = std::max(0, std::atoi(ev));  // A/B switch
   P.block_rot = 0;  // set at the launch (block rows of the launch's depth lanes)
   const size_t out_bytes = (size_t)P.plane_cols * (size_t)P.height * 3 * sizeof(float);
   if (d_out2) {
@@ -1250,9 +1350,9 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
   // LDS-staged march (vr_march.hip) whenever the emission texture is a real grid and, for the
   // on-the-fly gradient, is also the gradient texture; the plain kernel covers everything else.
   // Both produce bit-identical images (tests/test_gpu_parity.py::test_kernel_variants...).
-  const bool march = P.em.p && !P.em.one && (F.mode != 1 || F.share) && !env_flag("VR_NO_LDS");
+  const bool march = P.em.p && !P.em.one && (F.mode != 1 || F.share) && !test_flag("VR_NO_LDS");
   P.gvec = nullptr;
-  if (march && F.mode == 2 && F.share && !env_flag("VR_NO_GVEC")) {
+  if (march && F.mode == 2 && F.share && !test_flag("VR_NO_GVEC")) {
     // interleave the three gradient textures (one 16-byte load per voxel instead of three 4-byte
     // gathers from three volumes); without memory for it the kernel gathers them separately
     const BufPtr &bx = g_tex.bind[T_DX], &by = g_tex.bind[T_DY], &bz = g_tex.bind[T_DZ];
@@ -1303,7 +1403,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     // the counter variant: K = 1 (VR_COUNT_PROD=1 with a VR_COUNT_K=1 build: the production K's chunk
     // statistics; its sample sums are then 0)
     // (VR_COUNT_PROD is honoured by a VR_COUNT_K build only: a normal build has no counted K > 1 kernel)
-    const int K = (P.steps && !(VR_COUNT_K && env_flag("VR_COUNT_PROD"))) ? 1
+    const int K = (P.steps && !(VR_COUNT_K && test_flag("VR_COUNT_PROD"))) ? 1
                                                                           : exact_lanes(depth_lanes(P), P.fast_shade);
     set_chunk_halo(F, K);
     typedef hipError_t (*launch_fn)(const vr::RenderParams &, int, bool, bool, bool, hipStream_t);
@@ -1328,18 +1428,18 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       // column c + shift share a wave (and its staged box) with the right eye's of column c, the
       // shift (whole tiles) making the two bundles meet at the volume's centre, at distance `dist`
       // from the eyes: base * W * f / dist columns
-      if (env_flag("VR_STEREO_PAIR") && K > 1 && P.fast_shade && F.mode == 1 && F.ab_alias && P.tap_half &&
+      if (test_flag("VR_STEREO_PAIR") && K > 1 && P.fast_shade && F.mode == 1 && F.ab_alias && P.tap_half &&
           !P.wide_slot && !F.big && P.num_parts == 1 && !P.wg_order) {
         const double base = std::fabs((double)a->props[0]), f = std::fabs((double)a->props[1]),
                      dist = std::fabs((double)a->props[2]);
         const int TW = 4;  // tile width at K = 2, 4 (vr_march.hip TileShape)
         const double cols = dist > 0 ? base * (double)P.width * f / dist : 0.0;
         P.pair_shift = (int32_t)std::min<double>(std::floor(cols / TW + 0.5) * TW, (double)P.width);
-        if (const char *ev = std::getenv("VR_STEREO_PAIR_SHIFT")) P.pair_shift = std::max(0, std::atoi(ev));
+        if (const char *ev = test_env("VR_STEREO_PAIR_SHIFT")) P.pair_shift = std::max(0, std::atoi(ev));
       }
     }
     // diagnostics (VR_SCHED_DUMP): a timed launch also records its blocks' start ticks
-    const char *dump = (P.wg_cost && P.sched_full != 2) ? std::getenv("VR_SCHED_DUMP") : nullptr;
+    const char *dump = (P.wg_cost && P.sched_full != 2) ? test_env("VR_SCHED_DUMP") : nullptr;
     uint32_t *d_start = nullptr;
     if (dump) {
       const hipError_t e = hipMalloc(reinterpret_cast<void **>(&d_start), (size_t)P.sched_blocks * 4);
@@ -1348,7 +1448,7 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
     }
     // VR_BLOCK_ROT_ROWS=r (A/B): the unscheduled launch starts at block row r of the row-major order
     // and wraps (the light top rows then fill the ramp-down of the heavy middle band)
-    if (const char *ev = std::getenv("VR_BLOCK_ROT_ROWS")) {
+    if (const char *ev = test_env("VR_BLOCK_ROT_ROWS")) {
       const int TW = K == 1 ? 8 : (K == 2 ? 4 : (K == 4 ? 4 : 2));
       const uint32_t nbx = (uint32_t)((P.part_cols + 2 * TW - 1) / (2 * TW));
       typedef uint32_t (*bfn)(const vr::RenderParams &);
@@ -1539,7 +1639,7 @@ vr_host::EventPtr staged_copy(void *dst, int ddev, hipStream_t ds, const void *s
 // the device's group stream; a replica a launch still reads is replaced, not overwritten).
 BufPtr replicate(const BufPtr &b, int dev, hipStream_t s, bool peer = true) {
   if (!b) return b;
-  if (b->device == dev && !env_flag("VR_GROUP_REPLICATE")) return b;  // test switch: copy on one device too
+  if (b->device == dev && !test_flag("VR_GROUP_REPLICATE")) return b;  // test switch: copy on one device too
   BufPtr &r = b->replicas[dev];
   if (r && r->bytes == b->bytes && b->replica_of[dev] == b->version) return r;
   if (!(r && r->bytes == b->bytes && r->readers.done())) {
@@ -2196,7 +2296,7 @@ static int do_render_channels(const vr_channel *ch, int32_t n, int32_t stereo, f
   }
   const size_t img = (size_t)ch[0].args->resolution[0] * (size_t)ch[0].args->resolution[1] * 3;
   if (img && !d_out) return fail(VR_ERR_ARGUMENT, "output is NULL");
-  const bool fuse = !env_flag("VR_NO_FUSED_CHANNELS");
+  const bool fuse = !test_flag("VR_NO_FUSED_CHANNELS");
   vr_context *h0 = ch[0].handle;
   const int ndev = 1 + (int)h0->children.size();
   const int32_t bc = 16;
@@ -2723,6 +2823,14 @@ int64_t vr_hip_errors(char *buf, size_t buflen) {
     buf[n] = 0;
   }
   return (int64_t)L.count;
+}
+
+int vr_set_option(const char *name, int64_t value) {
+  if (name && std::strcmp(name, "test_switches") == 0) {
+    g_test_switches.store(value ? 1 : 0);
+    return VR_OK;
+  }
+  return fail(VR_ERR_ARGUMENT, std::string("unknown option ") + (name ? name : "(null)"));
 }
 
 int vr_last_march_kernel(char *buf, size_t buflen) {

@@ -620,31 +620,140 @@ __global__ void zpair_kernel(const float *src, float *dst, uint32_t n, uint32_t 
 // consecutive lanes then hold one brick.
 __global__ __launch_bounds__(256) void occupancy_kernel(const float *__restrict__ p, uint32_t px, uint32_t py,
                                                         uint32_t pz, uint8_t *__restrict__ occ, uint32_t obx,
-                                                        uint32_t oby) {
+                                                        uint32_t oby, float inv_scale) {
   constexpr uint32_t E = 1u << VR_OCC_LOG;  // brick edge
   const uint32_t x = blockIdx.x * 256u + threadIdx.x;
   const uint32_t by = blockIdx.y, bz = blockIdx.z;
   uint32_t acc = 0;
+  float sum = 0.f;
   if (x < px) {
     const uint64_t pxy = (uint64_t)px * py;
 #pragma unroll 8
     for (uint32_t k = 0; k < E * E; ++k) {
       const uint32_t y = by * E + (k & (E - 1)), z = bz * E + (k >> VR_OCC_LOG);
-      if (y < py && z < pz) acc |= __float_as_uint(p[(uint64_t)z * pxy + (uint64_t)y * px + x]) & 0x7fffffffu;
+      if (y < py && z < pz) {
+        const uint32_t u = __float_as_uint(p[(uint64_t)z * pxy + (uint64_t)y * px + x]) & 0x7fffffffu;
+        acc |= u;
+        sum += __uint_as_float(u);
+      }
     }
   }
 #pragma unroll
-  for (uint32_t m = 1; m < E; m <<= 1) acc |= (uint32_t)__shfl_xor((int)acc, (int)m, 64);
-  if ((threadIdx.x & (E - 1)) == 0 && x < px) occ[((uint64_t)bz * oby + by) * obx + (x >> VR_OCC_LOG)] = acc != 0u ? 1 : 0;
+  for (uint32_t m = 1; m < E; m <<= 1) {
+    acc |= (uint32_t)__shfl_xor((int)acc, (int)m, 64);
+    sum += __shfl_xor(sum, (int)m, 64);
+  }
+  // the byte: 0 iff every voxel is +-0 (what the probe tests); otherwise the brick's mean |voxel| in
+  // 1/255 of the volume's largest (1 at least; 255 for NaN / inf), the schedule predictor's density
+  if ((threadIdx.x & (E - 1)) == 0 && x < px) {
+    uint8_t q = 0;
+    if (acc != 0u) {
+      const float m = sum * (1.f / (float)(E * E * E)) * inv_scale;
+      q = (m == m && m < 254.5f) ? (uint8_t)fmaxf(1.f, ceilf(m)) : (uint8_t)255;
+    }
+    occ[((uint64_t)bz * oby + by) * obx + (x >> VR_OCC_LOG)] = q;
+  }
 }
 
-hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, hipStream_t s) {
+// inv_scale: 255 / the volume's largest |voxel| (0 if unknown: every occupied brick reads 1)
+hipError_t launch_occupancy(const float *p, uint32_t px, uint32_t py, uint32_t pz, uint8_t *occ, float inv_scale,
+                            hipStream_t s) {
   if (!px || !py || !pz) return hipSuccess;
   constexpr uint32_t E = 1u << VR_OCC_LOG;
   const uint32_t obx = (px + E - 1) / E, oby = (py + E - 1) / E, obz = (pz + E - 1) / E;
   if (oby > 65535 || obz > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(occupancy_kernel, dim3((px + 255) / 256, oby, obz), dim3(256), 0, s, p, px, py, pz, occ, obx,
-                     oby);
+                     oby, inv_scale);
+  return hipGetLastError();
+}
+
+// Predicted block costs (round 6, DESIGN.md s5 "history-free schedule"): the cost of march tile
+// block b (workgroup b of the launch; views x nb_view blocks, view-major) from the emission
+// texture's occupancy map alone -- no earlier frame of the same camera needed.  A block lasts as
+// long as its slowest wave; a wave iterates in lockstep over its rays' sample indices until its
+// last ray ends, and an iteration is cheap when none of its rays' samples is in an occupied brick
+// (the probe leaps up to 512 such samples at a time) and costly when any is (staged taps, gradient,
+// shading for the whole wave).  So one predictor wave per block walks 16 rays of each of the
+// block's four march waves (a 4 x 4 grid over each wave's tile) through the map in lockstep, m
+// samples (~8 texels) per step: per march wave it counts the steps where any of its rays is alive
+// and, VR_PRED_W_OCC times over, the steps where any of them is in an occupied brick; a ray ends at
+// its exit from the box or where the optical depth of the bricks' mean densities (Fa x mean |v| x
+// tstep per sample) reaches the early-exit threshold -log(1 - thr).  The block's cost is its most
+// costly wave's.  Only the order of the blocks follows from it: the image is the same for any order.
+#ifndef VR_PRED_W_OCC
+#define VR_PRED_W_OCC 16
+#endif
+__global__ __launch_bounds__(256) void predict_cost_kernel(const RenderParams P, uint32_t nb_view, uint32_t nbx,
+                                                           int32_t tw, int32_t th, int32_t m, float dens, float xthr,
+                                                           uint32_t *__restrict__ cost) {
+  const uint32_t b = (blockIdx.x * 256u + threadIdx.x) >> 6;  // the tile block (wave-uniform)
+  const int lane = (int)(threadIdx.x & 63u), q = lane >> 4, r = lane & 15;
+  const uint32_t nb = nb_view * (P.views > 1 ? 2u : 1u);
+  if (b >= nb) return;  // (whole waves)
+  const int view = b >= nb_view ? 1 : 0;
+  const uint32_t bb = view ? b - nb_view : b;
+  // march wave q of the block covers the tile (q & 1, q >> 1) of TW x TH pixels (vr_march.hip)
+  const int lc = (int)(bb % nbx) * 2 * tw + (q & 1) * tw + ((2 * (r & 3) + 1) * tw) / 8;
+  const int y = (int)(bb / nbx) * 2 * th + (q >> 1) * th + ((2 * (r >> 2) + 1) * th) / 8;
+  float ns = 0.f, g0x = 0.f, g0y = 0.f, g0z = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
+  if (lc < P.part_cols && y < P.height) {
+    const int pb = lc / P.block_cols;
+    const int x = (P.part + pb * P.num_parts) * P.block_cols + (lc - pb * P.block_cols);
+    f3 o, d;
+    float tnear, tfar;
+    if (ray_setup(P, x, y, o, d, tnear, tfar, view) && tfar >= tnear) {
+      ns = fminf(floorf((tfar - tnear) / P.tstep) + 1.f, (float)P.max_steps);
+      // texel coordinate + 1/2 per axis (its floor is the padded centre cell), at the first sample
+      // and per sample
+      const float sx = P.bscale[0] * P.em.fnx, sy = P.bscale[1] * P.em.fny, sz = P.bscale[2] * P.em.fnz;
+      g0x = fmaf(fmaf(d.x, tnear, o.x) - P.bmin[0], sx, 0.5f);
+      g0y = fmaf(fmaf(d.y, tnear, o.y) - P.bmin[1], sy, 0.5f);
+      g0z = fmaf(fmaf(d.z, tnear, o.z) - P.bmin[2], sz, 0.5f);
+      dx = d.x * P.tstep * sx;
+      dy = d.y * P.tstep * sy;
+      dz = d.z * P.tstep * sz;
+    }
+  }
+  const int obx = (int)P.occ_bx, oby = (int)(P.occ_bxy / P.occ_bx);
+  const int obz = (P.em.nz + 2 + (1 << VR_OCC_LOG) - 1) >> VR_OCC_LOG;
+  constexpr float inv = 1.f / (float)(1 << VR_OCC_LOG);
+  const float fm = (float)m;
+  float depth = 0.f, alive_s = 0.f, occ_s = 0.f;
+  const uint64_t gmask = 0xffffull << (16 * q);
+  for (float k0 = 0.f;; k0 += fm) {
+    const bool live = k0 < ns;
+    bool occ = false;
+    if (live) {
+      const float kc = fmaf(0.5f, fminf(fm, ns - k0), k0);
+      const int ix = min(max((int)floorf(fmaf(dx, kc, g0x) * inv), 0), obx - 1);
+      const int iy = min(max((int)floorf(fmaf(dy, kc, g0y) * inv), 0), oby - 1);
+      const int iz = min(max((int)floorf(fmaf(dz, kc, g0z) * inv), 0), obz - 1);
+      const uint32_t qv = P.occ[((uint32_t)iz * (uint32_t)oby + (uint32_t)iy) * (uint32_t)obx + (uint32_t)ix];
+      if (qv) {
+        occ = true;
+        depth = fmaf(dens * (float)qv, fm, depth);
+        if (depth > xthr) ns = k0;  // the ray's early exit, as far as the mean densities tell
+      }
+    }
+    const uint64_t lv = __ballot(live), oc = __ballot(occ);
+    if (lv == 0ull) break;
+    alive_s += (lv & gmask) ? fm : 0.f;
+    occ_s += (oc & gmask) ? fm : 0.f;
+  }
+  float c = fmaf(occ_s, (float)VR_PRED_W_OCC, alive_s) + 16.f;
+  c = fmaxf(c, __shfl_xor(c, 16, 64));
+  c = fmaxf(c, __shfl_xor(c, 32, 64));
+  if (lane == 0) cost[b] = (uint32_t)fminf(c, 4.0e9f);
+}
+
+// tw x th: the launch's march-wave tile in pixels (TW x TH of its depth lanes, vr_march.hip
+// TileShape); m: samples per predictor step
+hipError_t launch_predict_cost(const RenderParams &P, uint32_t nb_view, uint32_t nbx, int32_t tw, int32_t th,
+                               int32_t m, float dens, float xthr, uint32_t *cost, hipStream_t s) {
+  const uint64_t n = (uint64_t)nb_view * (P.views > 1 ? 2u : 1u);
+  if (!n || !P.occ || !P.occ_bx || P.part_cols <= 0 || P.height <= 0 || m < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(predict_cost_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, P, nb_view, nbx,
+                     tw, th, m, dens, xthr, cost);
   return hipGetLastError();
 }
 

@@ -165,6 +165,15 @@ struct ChunkStats {
 #ifndef VR_PROBE
 #define VR_PROBE 1  // the empty-space probe (vr_stage.h probe_run); 0: staged empty-chunk leaps only
 #endif
+#ifndef VR_PARK
+#define VR_PARK 1  // round 6: wave-front alignment of rays far apart along their direction (march)
+#endif
+#ifndef VR_PARK_SAMPLES
+#define VR_PARK_SAMPLES (2 * VR_CHUNK)  // parked: more than this many steps ahead of the wave's hindmost ray
+#endif
+#ifndef VR_PROBE_LANES
+#define VR_PROBE_LANES 1  // round 6: per-lane probes for waves whose rays are far apart (vr_stage.h probe_lanes)
+#endif
 #ifndef VR_PROBE_RETRY
 #define VR_PROBE_RETRY 1
 #endif
@@ -529,16 +538,21 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     if constexpr (PROBE) {
       if (ps > 0 && kp != nullptr && kparams_fresh(kp)->occ != nullptr) {
         const bool live = K > 1 ? (R.alive && R.mine) : R.alive;
-        int e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
+        // a box of too many bricks (the wave's rays far apart): each lane's own run (probe_lanes)
+        auto probe = [&](int len) __attribute__((always_inline)) {
+          const int r = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, len, lane);
+          return (VR_PROBE_LANES && r < 0) ? probe_lanes(P, kp, live, R.pos, R.step, R.t, R.tfar, len) : r;
+        };
+        int e = probe(ps);
         if (VR_PROBE_BISECT) {
           // an occupied (or too large) box: runs half as long until one is empty or the shortest fails
           while (e <= 0 && ps > VR_PROBE_MIN) {
             ps >>= 1;
-            e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
+            e = probe(ps);
           }
         } else if (VR_PROBE_RETRY && e < 0 && ps > VR_PROBE_MIN) {  // too many bricks: a run half as long
           ps >>= 1;
-          e = probe_run(P, kp, live, R.pos, R.step, R.t, R.tfar, ps, lane);
+          e = probe(ps);
         }
         if (e > 0) {
           if (COUNT) ++C.probe;
@@ -558,6 +572,40 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     bool edge = true;  // the box is clamped at a volume face (set by plan_chunk when it stages a whole box)
     plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial, B,
                     COUNT ? &box_vol : nullptr, &edge, s0);
+    // Wave-front alignment (round 6): when the chunk's box does not fit whole, the rays may be far
+    // apart along their direction rather than across it -- a tile whose rays enter the volume through
+    // a face at a grazing angle, or across an edge of the box, starts them up to hundreds of texels
+    // apart at the same sample index (45 texels at rotate(125,61,0), 420 at rotate(30,10,0)), and
+    // their chunks stage partially and gather from global memory.  All rays share the eye, so t is
+    // each ray's distance from it: the rays more than VR_PARK_SAMPLES steps ahead of the wave's
+    // hindmost are parked for this chunk (no box, no samples, no recurrence), and the box is planned
+    // for the others.  A parked ray's samples are taken later, by the same recurrence, so the image
+    // is the same; the hindmost ray always advances, so every ray finishes.
+    bool parked = false, keep_alive = R.alive, keep_mine = R.mine;
+    if constexpr (VR_PARK && !SLAB && !NANCHK) {
+      if (!staged || partial) {
+        const bool lv = K > 1 ? (R.alive && R.mine) : R.alive;
+        // (t >= 0 for every ray: its float bits order as integers)
+        const int tmin = wave_min(lv ? __float_as_int(R.t) : 0x7f7fffff);
+        bool pk = lv && R.t > __int_as_float(tmin) + (float)VR_PARK_SAMPLES * P.tstep;
+        if constexpr (K > 1) pk = group_any<K>(pk);  // (a ray's K lanes together)
+        if (__any(pk)) {
+          parked = pk;
+          if (parked) {
+            R.alive = false;
+            R.mine = false;
+          }
+          plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial,
+                          B, COUNT ? &box_vol : nullptr, &edge, s0);
+        }
+      }
+    }
+    auto unpark = [&]() __attribute__((always_inline)) {
+      if (parked) {
+        R.alive = keep_alive;
+        R.mine = keep_mine;
+      }
+    };
     if (VR_ADAPTIVE_S)
       s0 = (staged && !partial) ? min(2 * S, (int)VR_CHUNK) : (int)(VR_CHUNK >> (VR_ATTEMPTS - 1));
     bool inside = true;  // slab mode: every sample of this chunk lies in the slab
@@ -606,11 +654,15 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     const bool whole = __builtin_amdgcn_readfirstlane((!NANCHK && !SLAB && staged && !partial && !edge) ? 1 : 0) != 0;
 
     if (empty) {
-      leap_run(S);
+      if (!parked) leap_run(S);  // (the leap's additions are unconditional: not on a parked ray)
+      unpark();
       if (PROBE && ps < 0) ps = VR_PROBE_MIN;  // back in empty space after data: probe again
       continue;
     }
-    if (PROBE) ps = -1;  // data: armed
+    // data: armed; after a partial chunk (rays far apart, no chunk of theirs can be found empty by
+    // staging) the probe runs again before the next chunk -- one probe costs far less than a chunk of
+    // global gathers (VR_PROBE_LANES)
+    if (PROBE) ps = (VR_PROBE_LANES && partial) ? (int)VR_PROBE_MIN : -1;
 
     // ---- S samples ---------------------------------------------------------------------------
     if constexpr (K == 1) {
@@ -700,6 +752,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         samples(std::false_type{});
       }
     }
+    unpark();
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -1117,7 +1170,7 @@ hipError_t VR_CAT(launch_march_slab_k, VR_MARCH_K)(const RenderParams &P, int mo
 // a failed launch (tests/test_gpu_streams.py::test_failed_launch_is_reported_by_its_call).  Read
 // per launch.
 static bool inject_bad_launch() {
-  const char *ev = getenv("VR_INJECT_BAD_LAUNCH");
+  const char *ev = test_switches_on() ? getenv("VR_INJECT_BAD_LAUNCH") : nullptr;
   return ev && ev[0] == '1';
 }
 

@@ -548,7 +548,7 @@ struct Uploader {
   // src (host or device, per `on_device`) -> dst (padded, (nx+2)(ny+2)(nz+2) floats); *st = stats
   static bool timing() {
     static const bool on = [] {
-      const char *ev = std::getenv("VR_UPLOAD_TIMING");
+      const char *ev = vr::test_switches_on() ? std::getenv("VR_UPLOAD_TIMING") : nullptr;
       return ev && ev[0] == '1';
     }();
     return on;

@@ -507,6 +507,67 @@ __device__ __forceinline__ int probe_run(const RenderParams &P, KParams kp0, boo
   return __any(v != 0u) ? 0 : 1;
 }
 
+// Per-lane empty-space probe (round 6): whether every centre tap of each live lane's own next L
+// samples lies in +-0 bricks -- the test for waves whose rays are too far apart for one box
+// (probe_run's -1).  Rays that graze a volume face enter it at very different depths (a column of
+// pixels whose rays run almost parallel to the face: rotate(30,10,0) at 1920x1080, the 8 columns
+// next to the silhouette), so a wave's live rays spread along the face, its probe box spans
+// hundreds of bricks and its chunk boxes stage only partially: before round 6 such a block marched
+// its ~7000 empty samples per ray with global gathers, up to 55 ms.  Here each lane walks its own
+// run in segments of at most VR_LANE_SEG texels per axis; a segment's box (its end points' cells
+// widened by probe_off, as probe_run's box) spans at most 2 bricks per axis, whose bytes are ORed.
+// Consecutive segments share their end points bit for bit (both from the same expression), so the
+// segments cover the run's box end to end.  Returns 1 (all empty: leap) or 0.  Wave-uniform.
+#ifndef VR_LANE_SEG
+#define VR_LANE_SEG 4.0f
+#endif
+__device__ __forceinline__ int probe_lanes(const RenderParams &P, KParams kp0, bool alive, const f3 &pos,
+                                           const f3 &step, float t, float tfar, int L) {
+  // (every launch constant read through the argument segment at its point of use: the probe is rare,
+  // and values held for it across the sample loop would cost the loop registers)
+  const KParams kp = kparams_fresh(kp0);
+  uint32_t v = 0;
+  if (alive) {
+    const float rem = (tfar - t) / kp->tstep;  // as probe_run
+    const int s_eff = (rem < (float)L) ? max((int)rem + 2, 1) : L;
+    const float k = (float)(s_eff - 1);
+    const f3 pe = mk(fmaf(step.x, k, pos.x), fmaf(step.y, k, pos.y), fmaf(step.z, k, pos.z));
+    float a0[3], a1[3];
+    a0[0] = ((pos.x - kp->bmin[0]) * kp->bscale[0]) * kp->em.fnx - 0.5f;
+    a0[1] = ((pos.y - kp->bmin[1]) * kp->bscale[1]) * kp->em.fny - 0.5f;
+    a0[2] = ((pos.z - kp->bmin[2]) * kp->bscale[2]) * kp->em.fnz - 0.5f;
+    a1[0] = ((pe.x - kp->bmin[0]) * kp->bscale[0]) * kp->em.fnx - 0.5f;
+    a1[1] = ((pe.y - kp->bmin[1]) * kp->bscale[1]) * kp->em.fny - 0.5f;
+    a1[2] = ((pe.z - kp->bmin[2]) * kp->bscale[2]) * kp->em.fnz - 0.5f;
+    const float span = fmaxf(fabsf(a1[0] - a0[0]), fmaxf(fabsf(a1[1] - a0[1]), fabsf(a1[2] - a0[2])));
+    const int nseg = max(1, (int)ceilf(span * (1.f / VR_LANE_SEG)));
+    const float inv = 1.f / (float)nseg;
+    for (int j = 0; j < nseg && v == 0u; ++j) {
+      // segment j: from fraction j / nseg to (j + 1) / nseg of the run, per axis
+      const KParams kq = kparams_fresh(kp);
+      int blo[3], bhi[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const float s = a1[d] - a0[d];
+        const float c0 = j == 0 ? a0[d] : fmaf(s, (float)j * inv, a0[d]);
+        const float c1 = j + 1 == nseg ? a1[d] : fmaf(s, (float)(j + 1) * inv, a0[d]);
+        const int n = d == 0 ? kq->em.nx : (d == 1 ? kq->em.ny : kq->em.nz);
+        int lo, hi;
+        bool edge = false;
+        axis_range(c0, c1, kq->probe_off[d], n, lo, hi, edge);
+        blo[d] = lo >> VR_OCC_LOG;
+        bhi[d] = hi >> VR_OCC_LOG;
+      }
+      const uint8_t *occ = kq->occ;
+      const uint32_t obx = kq->occ_bx, obxy = kq->occ_bxy;
+      for (int bz = blo[2]; bz <= bhi[2]; ++bz)
+        for (int by = blo[1]; by <= bhi[1]; ++by)
+          for (int bx = blo[0]; bx <= bhi[0]; ++bx) v |= occ[(uint32_t)bz * obxy + (uint32_t)by * obx + (uint32_t)bx];
+    }
+  }
+  return __any(v != 0u) ? 0 : 1;
+}
+
 // The empty-chunk leap: every tap of the chunk lies in the staged all-zero box, so each sample has
 // em = ab = 0, alpha = 1 - exp(-0) = 0 and adds exactly 0 (skip_empty proves the shading term
 // finite).  Only the march recurrences run, in the reference's order.

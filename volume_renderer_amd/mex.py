@@ -232,6 +232,21 @@ def render_stereo_device(handle, ra: VrRenderArgs, base: float, d_left: int, d_r
                                         ctypes.c_void_p(int(stream)) if stream else None))
 
 
+def set_option(name: str, value: int) -> None:
+    """vr_set_option: a process-wide library option (include/vrhip.h)."""
+    check(lib().vr_set_option(name.encode(), int(value)))
+
+
+def enable_test_switches(on: bool = True) -> None:
+    """Let the library read the kernel-variant / schedule switches of the environment (VR_NO_LDS,
+    VR_DEPTH_LANES, VR_SCHED, ...; INTEGRATION.md "Runtime switches") -- the GPU tests and the
+    measurement tools; the MATLAB MEX never does, so a MATLAB session's environment cannot.  (An A/B
+    build of an earlier tree, VR_LIB_PATH, may predate the option: a DIAG=1 build reads them anyway.)"""
+    if not hasattr(lib(), "vr_set_option"):
+        return
+    set_option("test_switches", 1 if on else 0)
+
+
 def last_march_kernel() -> str:
     """The demangled name of the march kernel instantiation the last render launched."""
     buf = ctypes.create_string_buffer(256)
