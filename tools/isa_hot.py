@@ -10,7 +10,7 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/tmp/probe.s"
 s = open(path).read()
-name = re.search(r"(_ZN2vr4fast12march_kernelILi2ELi1ELb1ELb0ELb1ELb0ELi(?:1664|2040)ELi0EEEvNS_12RenderParamsE):", s).group(1)
+name = re.search(r"(_ZN2vr4fast12march_kernelILi2ELi1ELb1ELb0ELb1ELb0ELi(?:1664|2040)ELi0E(?:Li\d+E)?EEvNS_12RenderParamsE):", s).group(1)
 body = s[s.index(name + ":"):s.index(".Lfunc_end", s.index(name + ":"))].split("\n")
 blocks, cur = [], None
 for l in body:

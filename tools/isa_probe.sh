@@ -8,7 +8,7 @@ hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-mat
 python3 - <<'PY'
 import re, collections
 s = open('/tmp/probe.s').read()
-name = re.search(r'(_ZN2vr4fast12march_kernelILi2ELi1ELb1ELb0ELb1ELb0ELi(?:1664|2040)ELi0EEEvNS_12RenderParamsE):', s).group(1)
+name = re.search(r'(_ZN2vr4fast12march_kernelILi2ELi1ELb1ELb0ELb1ELb0ELi(?:1664|2040)ELi0E(?:Li\d+E)?EEvNS_12RenderParamsE):', s).group(1)
 body = s[s.index(name + ':'):s.index('.Lfunc_end', s.index(name + ':'))]
 ins = [l.strip().split()[0] for l in body.split('\n') if l.strip() and not l.strip().startswith(('.', ';')) and not l.strip().endswith(':')]
 c = collections.Counter(ins)

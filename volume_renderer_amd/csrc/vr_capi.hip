@@ -136,11 +136,12 @@ std::string &last_march_kernel() {
   return name;
 }
 
-void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched) {
+void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched,
+                       int nl) {
   char b[160];
   auto tf = [](bool v) { return v ? "true" : "false"; };
-  std::snprintf(b, sizeof b, "vr::%s::march_kernel<%d, %d, %s, %s, %s, %s, %d, %d>", fast ? "fast" : "exact", K, mode,
-                tf(ab), tf(count), tf(share), tf(big), cap, sched);
+  std::snprintf(b, sizeof b, "vr::%s::march_kernel<%d, %d, %s, %s, %s, %s, %d, %d, %d>", fast ? "fast" : "exact", K,
+                mode, tf(ab), tf(count), tf(share), tf(big), cap, sched, nl);
   last_march_kernel() = b;
 }
 }  // namespace vr

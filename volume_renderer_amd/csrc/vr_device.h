@@ -147,7 +147,8 @@ struct BufStats {
 // Host side: the demangled name of the march kernel a launch entry just enqueued (vr_capi.hip;
 // read back by vr_last_march_kernel, so that bench.py can name the kernel it times and match the
 // profiler's counters to exactly that instantiation).
-void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched);
+void note_march_kernel(bool fast, int K, int mode, bool ab, bool count, bool share, bool big, int cap, int sched,
+                       int nl);
 // Host side: whether vr_set_option("test_switches", 1) enabled the test-only environment switches.
 bool test_switches_on();
 

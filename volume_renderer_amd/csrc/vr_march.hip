@@ -165,6 +165,9 @@ struct ChunkStats {
 #ifndef VR_PROBE
 #define VR_PROBE 1  // the empty-space probe (vr_stage.h probe_run); 0: staged empty-chunk leaps only
 #endif
+#ifndef VR_NL2
+#define VR_NL2 1  // round 6: the two-light march specialised (march_kernel, shade_fast NL)
+#endif
 #ifndef VR_PARK
 #define VR_PARK 1  // round 6: wave-front alignment of rays far apart along their direction (march)
 #endif
@@ -190,7 +193,7 @@ struct ChunkStats {
 // One sample of a ray at position `pos` (volumeRender_kernel.cu:444-474): the emission /
 // absorption fetch, opacity, and for a lit, non-empty sample the gradient and the shading.  Returns
 // the premultiplied colour (r, g, b) and the opacity; `shaded` says whether shading ran.
-template <int MODE, bool AB_ALIAS, bool SHARE2, bool BIG, bool NANCHK>
+template <int MODE, bool AB_ALIAS, bool SHARE2, bool BIG, bool NANCHK, int NL = 0>
 __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L, const Box &B, bool staged, bool whole,
                                           const f3 pos, const f3 o, float &r, float &gg, float &b, float &alpha,
                                           bool &shaded, float rv = 0.f, const DevLight *pre = nullptr) {
@@ -360,7 +363,7 @@ __device__ __forceinline__ void sample_at(const RenderParams &P, const float *L,
     } else {
       refl = P.fr * (P.re_is_em ? em_s : tex3d<BIG>(P.re, ps.x, ps.y, ps.z));
     }
-    shade_lights<VR_MARCH_FAST, TAME>(P, g, pos, o, refl, ir, ig, ib, pre);
+    shade_lights<VR_MARCH_FAST, TAME, NL>(P, g, pos, o, refl, ir, ig, ib, pre);
   }
   r = fmaf(eds, P.color[0], ir) * alpha;
   gg = fmaf(eds, P.color[1], ig) * alpha;
@@ -470,7 +473,9 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 // has the position, t and step count of the one-volume march.  A ray stops here when it
 // terminates, or at its first sample beyond the slab in its direction of travel (`past`), whose
 // state becomes the resume point (store_resume).
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false>
+// NL: the launch's light count if the kernel is specialised on it (2; sample_at / shade_fast), else 0.
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false,
+          int NL = 0>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
                                       uint32_t kk = 0, KParams kp = nullptr) {
   static_assert(!COUNT || K == 1 || VR_COUNT_K, "the counter variant is built for K = 1 only (VR_COUNT_K: all K)");
@@ -513,13 +518,14 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
   // (only where the registers fit without lowering occupancy or spilling: not K = 1, the slab or
   // counter variants, nor the 64-bit, separate-absorption or full-gradient-tap ones)
   if constexpr (!NANCHK && VR_LIGHTS_HOIST && MODE != 0 && K > 1 && AB_ALIAS && SHARE2 && !BIG && !SLAB && !COUNT) {
-    const bool two = P.num_lights >= 2;
+    // (NL = 1: the single light in pre2[0])
+    const bool two = NL == 2 || (NL == 0 && P.num_lights >= 2);
     for (int j = 0; j < 2; ++j) {
-      pre2[j] = two ? light_at(P, j) : DevLight{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      pre2[j] = (two || (NL == 1 && j == 0)) ? light_at(P, j) : DevLight{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       asm volatile("" : "+v"(pre2[j].px), "+v"(pre2[j].py), "+v"(pre2[j].pz), "+v"(pre2[j].cr), "+v"(pre2[j].cg),
                    "+v"(pre2[j].cb));
     }
-    if (two) pre = pre2;
+    if (two || NL == 1) pre = pre2;
   }
   // the recurrences of n samples whose every sample adds exactly nothing (an empty-chunk leap or an
   // empty probe run); tame waves: one exit test after the n additions (advance_n; t only grows)
@@ -689,7 +695,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         }
         float r, gg, b, alpha;
         bool shaded;
-        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded,
+        sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK, NL>(P, L, B, staged, whole, R.pos, R.o, r, gg, b, alpha, shaded,
                                                        rv, pre);
         if (COUNT) {
           ++C.iter;
@@ -716,7 +722,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         }
         bool shaded = false;
         if (take) {
-          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK>(P, L, B, staged, WC || (!VR_WHOLE_SPLIT && whole), R.pos,
+          sample_at<MODE, AB_ALIAS, SHARE2, BIG, NANCHK, NL>(P, L, B, staged, WC || (!VR_WHOLE_SPLIT && whole), R.pos,
                                                          R.o, r, gg, b, alpha, shaded, rv, pre);
         }
         if (COUNT) {
@@ -823,7 +829,10 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n, int run) {
 // both eyes.  Columns are counted on a virtual image of part_cols + pair_shift columns: the left
 // eye's pixel at virtual column xv, the right eye's at xv - pair_shift; every pixel of each eye
 // is marched once.  Unpartitioned frames only.
-template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED>
+// NL (round 6, VR_NL2): 2 / 1 -- a launch of exactly two lights (the metric frame, examples/example1.m)
+// or one (examples/example2.m, example3.m), whose tame march shades the lights it holds in registers
+// without a light loop (shade_fast NL); 0 -- any light count.
+template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, int CAP, int SCHED, int NL>
 __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void march_kernel(const RenderParams P) {
   using TS = TileShape<K>;
   __shared__ float lds[VR_WG_WAVES][CAP];
@@ -887,7 +896,8 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   // every coordinate the march forms from a finite start and step is finite; a tame launch takes
   // the fast path (sample_at: TAME)
   if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP>(P, L, lane, R, C, 0u, (KParams)__builtin_amdgcn_kernarg_segment_ptr());
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP, false, NL>(P, L, lane, R, C, 0u,
+                                                                          (KParams)__builtin_amdgcn_kernarg_segment_ptr());
   else
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
@@ -1174,6 +1184,18 @@ static bool inject_bad_launch() {
   return ev && ev[0] == '1';
 }
 
+// One march_kernel launch; a lit launch of one or two lights takes the NL = 1 / 2 kernel where the
+// lights are hoisted (march: VR_LIGHTS_HOIST's conditions).
+template <int KK, int MODE, bool AB, bool CNT, bool SH, bool BG, int CAP, int SC>
+static void launch_one(const RenderParams &P, dim3 grid, dim3 blk, hipStream_t s) {
+  constexpr bool NL2 = VR_NL2 && VR_LIGHTS_HOIST && MODE != 0 && KK > 1 && AB && SH && !BG && !CNT;
+  const int nl = (NL2 && (P.num_lights == 2 || P.num_lights == 1)) ? P.num_lights : 0;
+  if (NL2 && nl == 2) hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC, NL2 ? 2 : 0>), grid, blk, 0, s, P);
+  else if (NL2 && nl == 1) hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC, NL2 ? 1 : 0>), grid, blk, 0, s, P);
+  else hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC, 0>), grid, blk, 0, s, P);
+  note_march_kernel(VR_MARCH_FAST, KK, MODE, AB, CNT, SH, BG, CAP, SC, nl);
+}
+
 // BS: the addressing variants this instantiation holds (1: 32-bit, 2: 64-bit, 3: both) -- the
 // narrow slot differs between them (launch_m), the kernel count does not.
 template <int MODE, bool AB, bool SH, int CAP, int BS = 3>
@@ -1185,11 +1207,7 @@ static hipError_t launch_c(const RenderParams &P, dim3 grid, hipStream_t s, bool
   // alias the SCHED 0 kernel; the host schedules no other launch, vr_capi.hip attach_schedule)
   constexpr bool SCH = K > 1 && VR_MARCH_FAST && AB;
   constexpr int S1 = SCH ? 1 : 0, S2 = SCH ? 2 : 0, S3 = SCH ? 3 : 0;
-#define VR_LAUNCH(KK, CNT, BG, SC)                                                                         \
-  do {                                                                                                    \
-    hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC>), grid, blk, 0, s, P);          \
-    note_march_kernel(VR_MARCH_FAST, KK, MODE, AB, CNT, SH, BG, CAP, SC);                                 \
-  } while (0)
+#define VR_LAUNCH(KK, CNT, BG, SC) launch_one<KK, MODE, AB, CNT, SH, BG, CAP, SC>(P, grid, blk, s)
 #define VR_LAUNCH_B(KK, CNT, SC)                                                                           \
   do {                                                                                                    \
     if (big) {                                                                                            \
@@ -1297,8 +1315,8 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
 #else
 // ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation and the matching
 // sort-last slab kernel, for a quick look at their code without compiling every variant.
-template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP_MARCH, 0>(const RenderParams P);
-template __global__ void march_kernel<2, 2, true, false, true, false, VR_LDS_CAP, 0>(const RenderParams P);  // C3
+template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP_MARCH, 0, 2>(const RenderParams P);
+template __global__ void march_kernel<2, 2, true, false, true, false, VR_LDS_CAP, 0, 2>(const RenderParams P);  // C3
 template __global__ void march_slab_kernel<2, 1, true, VR_LDS_CAP, false>(const RenderParams P);
 #endif  // !VR_ISA_PROBE
 }  // namespace fast / exact

@@ -689,10 +689,16 @@ __device__ __forceinline__ float voxel0(const float *p) {
 // within asin(sqrt(VR_HYB_TA)) of the normal (its projection onto the tangent plane cancels, so the
 // normal's last bits decide its direction) or a gamma cosine beyond +-VR_HYB_TG (acos amplifies the
 // cosine's rounding there) -- where the hybrid shading (VR_FAST_HYBRID) takes XN + XG.
-template <bool TAME, bool XN, bool XG, bool NEED>
+// NL (round 6): the launch's light count when the kernel was specialised on it (2: the metric frame
+// and examples/example1.m; 1: examples/example2.m and example3.m -- the lights are the caller's
+// hoisted `pre`, no light loop, no masks of the loop bounds held across the sample loop); 0:
+// P.num_lights.
+template <bool TAME, bool XN, bool XG, bool NEED, int NL = 0>
 __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                           const float refl, float &ir, float &ig, float &ib, bool &need,
                                           const DevLight *pre = nullptr) {
+  static_assert(NL == 0 || ((NL == 1 || NL == 2) && TAME), "specialised for hoisted lights only");
+  const int nl = NL ? NL : P.num_lights;
   // n = -g * rsq(g.g): rsq(0) = inf gives the reference's NaN normal for a zero gradient
   float ginv;
   if constexpr (XN) ginv = rcp_sqrt_cr(dot3(g, g));  // the oracle's 1 / sqrtf(g.g), bit for bit
@@ -742,10 +748,10 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
   if (TAME || (P.lut.p != nullptr && P.lut.small && !P.lut.one)) {
     // the common LUT (bound, below 2^22 padded voxels): one wave-uniform test for the frame's
     // lights; a pair's eight LUT row loads are issued together, ahead of their lerps
-    for (; i + 1 < P.num_lights; i += 2) {
+    for (; i + 1 < nl; i += 2) {
       // pre: the first pair held in registers by the caller (vr_march.hip VR_LIGHTS_HOIST)
-      const DevLight L0 = (pre && i == 0) ? pre[0] : light_at(P, i);
-      const DevLight L1 = (pre && i == 0) ? pre[1] : light_at(P, i + 1);
+      const DevLight L0 = NL == 2 ? pre[0] : ((pre && i == 0) ? pre[0] : light_at(P, i));
+      const DevLight L1 = NL == 2 ? pre[1] : ((pre && i == 0) ? pre[1] : light_at(P, i + 1));
       const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
       const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
       const float dlo0 = dot3(lo0, n), dlo1 = dot3(lo1, n);
@@ -777,7 +783,7 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
       ib = fmaf(rl1 * L1.cb, P.color[2], ib);
     }
   }
-  if constexpr (!TAME) for (; i + 1 < P.num_lights; i += 2) {
+  if constexpr (!TAME) for (; i + 1 < nl; i += 2) {
     const DevLight L0 = light_at(P, i), L1 = light_at(P, i + 1);
     const f3 lo0 = mk(L0.px - pos.x, L0.py - pos.y, L0.pz - pos.z);
     const f3 lo1 = mk(L1.px - pos.x, L1.py - pos.y, L1.pz - pos.z);
@@ -799,8 +805,8 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
     ig = fmaf(rl1 * L1.cg, P.color[1], ig);
     ib = fmaf(rl1 * L1.cb, P.color[2], ib);
   }
-  if (i < P.num_lights) {
-    const DevLight L = light_at(P, i);
+  if (i < nl) {
+    const DevLight L = NL == 1 ? pre[0] : light_at(P, i);
     const f3 lo = mk(L.px - pos.x, L.py - pos.y, L.pz - pos.z);
     const float dlo = dot3(lo, n);
     const f3 lop = mk(fmaf(-dlo, n.x, lo.x), fmaf(-dlo, n.y, lo.y), fmaf(-dlo, n.z, lo.z));
@@ -817,7 +823,7 @@ __device__ __forceinline__ void shade_fast(const RenderParams &P, const f3 g, co
   }
 }
 
-template <bool FAST, bool TAME = false>
+template <bool FAST, bool TAME = false, int NL = 0>
 __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, const f3 pos, const f3 o,
                                              const float refl, float &ir, float &ig, float &ib,
                                              const DevLight *pre = nullptr) {
@@ -879,7 +885,7 @@ __device__ __forceinline__ void shade_lights(const RenderParams &P, const f3 g, 
     }
 #else
     bool unused = false;
-    shade_fast<TAME, VR_FAST_NX, VR_FAST_GX, false>(P, g, pos, o, refl, ir, ig, ib, unused, pre);
+    shade_fast<TAME, VR_FAST_NX, VR_FAST_GX, false, NL>(P, g, pos, o, refl, ir, ig, ib, unused, pre);
 #endif
   } else {
     // surface normal n = -normalize(g); normalize(0) = 0 * inf = NaN as in the reference.

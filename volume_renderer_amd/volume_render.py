@@ -179,16 +179,15 @@ class VolumeRender:
         return self._compose(left, right, delta)
 
     def _fused_stereo(self) -> bool:
-        """Both eyes in one launch where it pays: on a device group (VR_DEVICES), whose per-device
-        column parts are too small to fill a GPU on their own; on one GPU each eye fills it and the
-        fused launch measured slower than two renders (84.2 vs 82.9 ms), so the
-        reference's two renders are the default there.  VR_FUSED_STEREO=1 / VR_NO_FUSED_STEREO=1
-        force either way.  The images are bit-identical either way."""
+        """Both eyes in one launch (vr_render_stereo), the default since round 6: on one GPU the
+        fused launch, scheduled over both views' blocks, measured 82.05 vs 84.01 ms for the
+        reference's two renders at C4's stereo geometry (profiles/round6/stereo_pair.json; round 5:
+        75.8 vs 78.3), and on a device group (VR_DEVICES) each device's column parts are too small to
+        fill it alone.  VR_NO_FUSED_STEREO=1 restores the two renders (VR_FUSED_STEREO=1 is accepted
+        as before).  The images are bit-identical either way."""
         if os.environ.get("VR_NO_FUSED_STEREO") == "1":
             return False
-        if os.environ.get("VR_FUSED_STEREO") == "1":
-            return True
-        return bool(getattr(self, "_group", False))
+        return True
 
     def _compose(self, left, right, delta):
         """VolumeRender.m:288-307: crop the eyes, red-cyan anaglyph or side by side."""
