@@ -174,11 +174,18 @@ struct ChunkStats {
 #ifndef VR_PARK_SAMPLES
 #define VR_PARK_SAMPLES (2 * VR_CHUNK)  // parked: more than this many steps ahead of the wave's hindmost ray
 #endif
-#ifndef VR_PROBE_LANES
-#define VR_PROBE_LANES 1  // round 6: per-lane probes for waves whose rays are far apart (vr_stage.h probe_lanes)
+#ifndef VR_REPROBE_PARTIAL
+#define VR_REPROBE_PARTIAL 1  // after a partial chunk the probe runs again before the next chunk
 #endif
-#ifndef VR_PROBE_RETRY
-#define VR_PROBE_RETRY 1
+#ifndef VR_PRELEAP
+#define VR_PRELEAP 1  // round 6: per-lane leaps of empty runs before the march of a wave whose rays are far apart
+#endif
+#ifndef VR_PRELEAP_SPREAD
+#define VR_PRELEAP_SPREAD 256  // ... more than this many steps apart (the grazing tiles of rotate(30,10,0): 900-2700)
+#endif
+#ifndef VR_PROBE_LANES
+#define VR_PROBE_LANES 0  // round 6: per-lane probes inside the march loop for waves whose rays are far apart
+                          // (vr_stage.h probe_lanes; measured: +0.4 ms metric, +1.2 ms C3 -- VR_PRELEAP instead)
 #endif
 #ifndef VR_PROBE_BISECT
 // 1: a probe that finds data (or too many bricks) retries at half the run length, down to
@@ -540,6 +547,55 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       R.alive = R.alive && group_any<K>(R.mine);
     }
   };
+  // Per-lane pre-leap (round 6, VR_PRELEAP): a wave whose rays start far apart along their direction
+  // (t spread beyond VR_PRELEAP_SPREAD steps: a tile of rays entering the volume through a face at a
+  // grazing angle) cannot probe one box for them all, so before the march each ray walks the
+  // occupancy map along its own runs of VR_PROBE_MAX samples (probe_lane_walk) and leaps every run
+  // whose centre cells all lie in +-0 bricks -- exact as the probe's leap, run by run (the margin
+  // covers one run's drift) -- until a run finds data; a ray's K lanes leap together.  Rays that
+  // only graze empty space (rotate(30,10,0): the columns next to the silhouette, ~7000 empty samples
+  // each) end here; the rest start at their data, where wave-front parking aligns them.
+  if constexpr (PROBE && VR_PRELEAP && !COUNT) {
+    if (kp != nullptr && kparams_fresh(kp)->occ != nullptr) {
+      const bool lv0 = K > 1 ? (R.alive && R.mine) : R.alive;
+      const int tmn = wave_min(lv0 ? __float_as_int(R.t) : 0x7f7fffff);
+      const int tmx = wave_max(lv0 ? __float_as_int(R.t) : 0);
+      if (__int_as_float(tmx) > __int_as_float(tmn) + (float)VR_PRELEAP_SPREAD * P.tstep) {
+        bool go = lv0;
+        while (group_any<K>(go)) {  // (a ray's K lanes decide together)
+          const KParams kq = kparams_fresh(kp);
+          uint32_t v = 0;
+          if (go) {
+            const float rem = (R.tfar - R.t) / kq->tstep;
+            const int s_eff = (rem < (float)VR_PROBE_MAX) ? max((int)rem + 2, 1) : (int)VR_PROBE_MAX;
+            const float k = (float)(s_eff - 1);
+            const f3 pe = mk(fmaf(R.step.x, k, R.pos.x), fmaf(R.step.y, k, R.pos.y), fmaf(R.step.z, k, R.pos.z));
+            v = probe_lane_walk(kq->occ, kq->occ_bx, kq->occ_bxy,
+                                ((R.pos.x - kq->bmin[0]) * kq->bscale[0]) * kq->em.fnx - 0.5f,
+                                ((R.pos.y - kq->bmin[1]) * kq->bscale[1]) * kq->em.fny - 0.5f,
+                                ((R.pos.z - kq->bmin[2]) * kq->bscale[2]) * kq->em.fnz - 0.5f,
+                                ((pe.x - kq->bmin[0]) * kq->bscale[0]) * kq->em.fnx - 0.5f,
+                                ((pe.y - kq->bmin[1]) * kq->bscale[1]) * kq->em.fny - 0.5f,
+                                ((pe.z - kq->bmin[2]) * kq->bscale[2]) * kq->em.fnz - 0.5f, kq->probe_off[0],
+                                kq->probe_off[1], kq->probe_off[2], kq->em.nx, kq->em.ny, kq->em.nz);
+          }
+          const bool data = group_any<K>(v != 0u);
+          if (go && !data) {
+            if constexpr (K == 1) {
+              advance_n(P, (int)VR_PROBE_MAX, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+              go = R.alive;
+            } else {
+              advance_n(P, (int)VR_PROBE_MAX, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+              go = group_any<K>(R.mine);
+            }
+          } else {
+            go = false;
+          }
+        }
+        if constexpr (K > 1) R.alive = R.alive && group_any<K>(R.mine);
+      }
+    }
+  }
   while (__any(R.alive)) {
     if constexpr (PROBE) {
       if (ps > 0 && kp != nullptr && kparams_fresh(kp)->occ != nullptr) {
@@ -550,13 +606,8 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
           return (VR_PROBE_LANES && r < 0) ? probe_lanes(P, kp, live, R.pos, R.step, R.t, R.tfar, len) : r;
         };
         int e = probe(ps);
-        if (VR_PROBE_BISECT) {
-          // an occupied (or too large) box: runs half as long until one is empty or the shortest fails
-          while (e <= 0 && ps > VR_PROBE_MIN) {
-            ps >>= 1;
-            e = probe(ps);
-          }
-        } else if (VR_PROBE_RETRY && e < 0 && ps > VR_PROBE_MIN) {  // too many bricks: a run half as long
+        // an occupied (or too large) box: runs half as long until one is empty or the shortest fails
+        while (VR_PROBE_BISECT && e <= 0 && ps > VR_PROBE_MIN) {
           ps >>= 1;
           e = probe(ps);
         }
@@ -587,7 +638,10 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     // hindmost are parked for this chunk (no box, no samples, no recurrence), and the box is planned
     // for the others.  A parked ray's samples are taken later, by the same recurrence, so the image
     // is the same; the hindmost ray always advances, so every ray finishes.
-    bool parked = false, keep_alive = R.alive, keep_mine = R.mine;
+    // (a parked ray's mark is the sign of its t -- t >= 0 otherwise -- so that nothing per lane is
+    // held across the sample loop; it has alive = false meanwhile, and every lane of a parked ray's
+    // group is parked, so no group operation of the chunk reads it)
+    bool parked_any = false;  // wave-uniform
     if constexpr (VR_PARK && !SLAB && !NANCHK) {
       if (!staged || partial) {
         const bool lv = K > 1 ? (R.alive && R.mine) : R.alive;
@@ -596,10 +650,10 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
         bool pk = lv && R.t > __int_as_float(tmin) + (float)VR_PARK_SAMPLES * P.tstep;
         if constexpr (K > 1) pk = group_any<K>(pk);  // (a ray's K lanes together)
         if (__any(pk)) {
-          parked = pk;
-          if (parked) {
+          parked_any = true;
+          if (pk) {
             R.alive = false;
-            R.mine = false;
+            R.t = -R.t;
           }
           plan_chunk<CAP>(P, K > 1 ? (R.alive && R.mine) : R.alive, R.pos, R.step, R.t, R.tfar, S, staged, partial,
                           B, COUNT ? &box_vol : nullptr, &edge, s0);
@@ -607,9 +661,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       }
     }
     auto unpark = [&]() __attribute__((always_inline)) {
-      if (parked) {
-        R.alive = keep_alive;
-        R.mine = keep_mine;
+      if (parked_any && __float_as_int(R.t) < 0) {  // (-0 too)
+        R.t = -R.t;
+        R.alive = true;
       }
     };
     if (VR_ADAPTIVE_S)
@@ -660,7 +714,9 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     const bool whole = __builtin_amdgcn_readfirstlane((!NANCHK && !SLAB && staged && !partial && !edge) ? 1 : 0) != 0;
 
     if (empty) {
-      if (!parked) leap_run(S);  // (the leap's additions are unconditional: not on a parked ray)
+      // (the leap's additions are unconditional: not on a parked ray)
+      if (!parked_any) leap_run(S);
+      else if (__float_as_int(R.t) >= 0) leap_run(S);
       unpark();
       if (PROBE && ps < 0) ps = VR_PROBE_MIN;  // back in empty space after data: probe again
       continue;
@@ -668,7 +724,7 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
     // data: armed; after a partial chunk (rays far apart, no chunk of theirs can be found empty by
     // staging) the probe runs again before the next chunk -- one probe costs far less than a chunk of
     // global gathers (VR_PROBE_LANES)
-    if (PROBE) ps = (VR_PROBE_LANES && partial) ? (int)VR_PROBE_MIN : -1;
+    if (PROBE) ps = (VR_PROBE_LANES && VR_REPROBE_PARTIAL && partial) ? (int)VR_PROBE_MIN : -1;
 
     // ---- S samples ---------------------------------------------------------------------------
     if constexpr (K == 1) {

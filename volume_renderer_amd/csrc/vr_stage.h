@@ -521,6 +521,47 @@ __device__ __forceinline__ int probe_run(const RenderParams &P, KParams kp0, boo
 #ifndef VR_LANE_SEG
 #define VR_LANE_SEG 4.0f
 #endif
+// The walk of one lane (no wave operations inside, every launch constant an argument).  Inlined it
+// weighs on the sample loop of every launch although it rarely runs (round 6, same box: metric frame
+// 25.34-25.40 vs 24.89-25.00 ms without the lane probe, C3 28.8-28.9 vs 27.5-27.7); out of line
+// (VR_PROBE_LANES_CALL=1) the call's register saves spill more (metric kernel 5 VGPRs), so inline.
+#ifndef VR_PROBE_LANES_CALL
+#define VR_PROBE_LANES_CALL 0
+#endif
+#if VR_PROBE_LANES_CALL
+#define VR_LANES_ATTR __attribute__((noinline))
+#else
+#define VR_LANES_ATTR __forceinline__
+#endif
+__device__ VR_LANES_ATTR uint32_t probe_lane_walk(const uint8_t *occ, uint32_t obx, uint32_t obxy, float a0x, float a0y,
+                                                  float a0z, float a1x, float a1y, float a1z, float ox, float oy,
+                                                  float oz, int nx, int ny, int nz) {
+  const float a0[3] = {a0x, a0y, a0z}, a1[3] = {a1x, a1y, a1z}, off[3] = {ox, oy, oz};
+  const int n[3] = {nx, ny, nz};
+  const float span = fmaxf(fabsf(a1x - a0x), fmaxf(fabsf(a1y - a0y), fabsf(a1z - a0z)));
+  const int nseg = max(1, (int)ceilf(span * (1.f / VR_LANE_SEG)));
+  const float inv = 1.f / (float)nseg;
+  uint32_t v = 0;
+  for (int j = 0; j < nseg && v == 0u; ++j) {
+    // segment j: from fraction j / nseg to (j + 1) / nseg of the run, per axis
+    int blo[3], bhi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const float s = a1[d] - a0[d];
+      const float c0 = j == 0 ? a0[d] : fmaf(s, (float)j * inv, a0[d]);
+      const float c1 = j + 1 == nseg ? a1[d] : fmaf(s, (float)(j + 1) * inv, a0[d]);
+      int lo, hi;
+      bool edge = false;
+      axis_range(c0, c1, off[d], n[d], lo, hi, edge);
+      blo[d] = lo >> VR_OCC_LOG;
+      bhi[d] = hi >> VR_OCC_LOG;
+    }
+    for (int bz = blo[2]; bz <= bhi[2]; ++bz)
+      for (int by = blo[1]; by <= bhi[1]; ++by)
+        for (int bx = blo[0]; bx <= bhi[0]; ++bx) v |= occ[(uint32_t)bz * obxy + (uint32_t)by * obx + (uint32_t)bx];
+  }
+  return v;
+}
 __device__ __forceinline__ int probe_lanes(const RenderParams &P, KParams kp0, bool alive, const f3 &pos,
                                            const f3 &step, float t, float tfar, int L) {
   // (every launch constant read through the argument segment at its point of use: the probe is rare,
@@ -532,38 +573,14 @@ __device__ __forceinline__ int probe_lanes(const RenderParams &P, KParams kp0, b
     const int s_eff = (rem < (float)L) ? max((int)rem + 2, 1) : L;
     const float k = (float)(s_eff - 1);
     const f3 pe = mk(fmaf(step.x, k, pos.x), fmaf(step.y, k, pos.y), fmaf(step.z, k, pos.z));
-    float a0[3], a1[3];
-    a0[0] = ((pos.x - kp->bmin[0]) * kp->bscale[0]) * kp->em.fnx - 0.5f;
-    a0[1] = ((pos.y - kp->bmin[1]) * kp->bscale[1]) * kp->em.fny - 0.5f;
-    a0[2] = ((pos.z - kp->bmin[2]) * kp->bscale[2]) * kp->em.fnz - 0.5f;
-    a1[0] = ((pe.x - kp->bmin[0]) * kp->bscale[0]) * kp->em.fnx - 0.5f;
-    a1[1] = ((pe.y - kp->bmin[1]) * kp->bscale[1]) * kp->em.fny - 0.5f;
-    a1[2] = ((pe.z - kp->bmin[2]) * kp->bscale[2]) * kp->em.fnz - 0.5f;
-    const float span = fmaxf(fabsf(a1[0] - a0[0]), fmaxf(fabsf(a1[1] - a0[1]), fabsf(a1[2] - a0[2])));
-    const int nseg = max(1, (int)ceilf(span * (1.f / VR_LANE_SEG)));
-    const float inv = 1.f / (float)nseg;
-    for (int j = 0; j < nseg && v == 0u; ++j) {
-      // segment j: from fraction j / nseg to (j + 1) / nseg of the run, per axis
-      const KParams kq = kparams_fresh(kp);
-      int blo[3], bhi[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const float s = a1[d] - a0[d];
-        const float c0 = j == 0 ? a0[d] : fmaf(s, (float)j * inv, a0[d]);
-        const float c1 = j + 1 == nseg ? a1[d] : fmaf(s, (float)(j + 1) * inv, a0[d]);
-        const int n = d == 0 ? kq->em.nx : (d == 1 ? kq->em.ny : kq->em.nz);
-        int lo, hi;
-        bool edge = false;
-        axis_range(c0, c1, kq->probe_off[d], n, lo, hi, edge);
-        blo[d] = lo >> VR_OCC_LOG;
-        bhi[d] = hi >> VR_OCC_LOG;
-      }
-      const uint8_t *occ = kq->occ;
-      const uint32_t obx = kq->occ_bx, obxy = kq->occ_bxy;
-      for (int bz = blo[2]; bz <= bhi[2]; ++bz)
-        for (int by = blo[1]; by <= bhi[1]; ++by)
-          for (int bx = blo[0]; bx <= bhi[0]; ++bx) v |= occ[(uint32_t)bz * obxy + (uint32_t)by * obx + (uint32_t)bx];
-    }
+    v = probe_lane_walk(kp->occ, kp->occ_bx, kp->occ_bxy,
+                        ((pos.x - kp->bmin[0]) * kp->bscale[0]) * kp->em.fnx - 0.5f,
+                        ((pos.y - kp->bmin[1]) * kp->bscale[1]) * kp->em.fny - 0.5f,
+                        ((pos.z - kp->bmin[2]) * kp->bscale[2]) * kp->em.fnz - 0.5f,
+                        ((pe.x - kp->bmin[0]) * kp->bscale[0]) * kp->em.fnx - 0.5f,
+                        ((pe.y - kp->bmin[1]) * kp->bscale[1]) * kp->em.fny - 0.5f,
+                        ((pe.z - kp->bmin[2]) * kp->bscale[2]) * kp->em.fnz - 0.5f, kp->probe_off[0],
+                        kp->probe_off[1], kp->probe_off[2], kp->em.nx, kp->em.ny, kp->em.nz);
   }
   return __any(v != 0u) ? 0 : 1;
 }
