@@ -211,3 +211,29 @@ def test_test_switches_are_off_by_default(monkeypatch, counter_clock):
     with pytest.raises(Exception):
         mex.set_option("no_such_option", 1)
     r.delete()
+
+
+@pytest.mark.parametrize("lanes", ["2", "4"])
+def test_preleap_launch_keeps_the_image(monkeypatch, counter_clock, lanes):
+    """The pre-leap launch (vr_march.hip preleap_kernel): at rotate(30,10,0) the columns next to the
+    silhouette run almost parallel to the x = -1 face, so their tiles' rays start hundreds of samples
+    apart and are pre-leaped through the occupancy map before the march.  The frames equal, bit for
+    bit, those without the pre-leap (VR_NO_PRELEAP=1) and the unscheduled ones (VR_SCHED=0: no
+    schedule, no pre-leap launch), at either depth-lane count."""
+    monkeypatch.setenv("VR_DEPTH_LANES", lanes)
+    v = vr.Volume(O.shell_volume(128))
+    out = {}
+    for mode, env in (("default", {}), ("nopre", {"VR_NO_PRELEAP": "1"}), ("plain", {"VR_SCHED": "0"})):
+        for k in ("VR_NO_PRELEAP", "VR_SCHED"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        r = renderer(v, res=(1024, 1024), rot=(30, 10, 0))
+        out[mode] = [r.render()]
+        r.rotate(0, 12, 0)
+        out[mode].append(r.render())
+        r.delete()
+    for mode in ("nopre", "plain"):
+        for a, b in zip(out["default"], out[mode]):
+            assert a.max() > 0
+            assert np.array_equal(bits(a), bits(b)), mode

@@ -65,6 +65,10 @@ hipError_t launch_render(const RenderParams &P, int mode, bool ab_alias, bool bi
   uint32_t march_blocks_k2(const RenderParams &);                                                        \
   uint32_t march_blocks_k4(const RenderParams &);                                                        \
   uint32_t march_blocks_k8(const RenderParams &);                                                        \
+  hipError_t launch_preleap_k1(const RenderParams &, hipStream_t);                                       \
+  hipError_t launch_preleap_k2(const RenderParams &, hipStream_t);                                       \
+  hipError_t launch_preleap_k4(const RenderParams &, hipStream_t);                                       \
+  hipError_t launch_preleap_k8(const RenderParams &, hipStream_t);                                       \
   }
 VR_DECL_MARCH(fast)
 VR_DECL_MARCH(exact)
@@ -122,6 +126,10 @@ hipError_t launch_resize_dim(const float *in, const uint64_t dims[3], int dim, u
 #define VR_DEPTH_TAU_K1 0.5      // K = 1 (with >= VR_DEPTH_ROUNDS_K1 rounds) below this many
 #endif
 
+#ifndef VR_PRELEAP_LAUNCH
+#define VR_PRELEAP_LAUNCH 1  // round 6: the pre-leap launch before scheduled tame marches (vr_march.hip preleap_kernel)
+#endif
+#define VR_WG_WAVES_HOST 4  // waves per march workgroup (vr_march.hip VR_WG_WAVES)
 #ifndef VR_SCHED_ROUNDS
 #define VR_SCHED_ROUNDS 6.0      // longest-first schedule below this many K = 1 waves per wave slot
 #endif
@@ -269,6 +277,11 @@ struct vr_context {
     // round 6: the frame (camera, volume upload, opacity parameters, frame_key) the durations were
     // measured on, and the one the order in d_order was predicted for (0: none)
     uint64_t key = 0, pred_key = 0;
+    // round 6: the pre-leap launch's buffers (vr_march.hip preleap_kernel): a flag per march wave,
+    // ray-state slots for pre_cap waves, the slot counter
+    uint32_t *pre_flag = nullptr, *pre_count = nullptr;
+    float4 *pre_state = nullptr;
+    uint32_t pre_waves = 0, pre_cap = 0;
   };
   std::map<std::string, Schedule> sched;
   // vr_render_channels: the views' RenderParams and lights in device memory (reused per call)
@@ -946,6 +959,9 @@ void free_schedules(vr_context *h) {
     if (kv.second.d_cost) (void)hipFree(kv.second.d_cost);
     if (kv.second.d_order) (void)hipFree(kv.second.d_order);
     if (kv.second.h_cost) (void)hipHostFree(kv.second.h_cost);
+    if (kv.second.pre_flag) (void)hipFree(kv.second.pre_flag);
+    if (kv.second.pre_count) (void)hipFree(kv.second.pre_count);
+    if (kv.second.pre_state) (void)hipFree(kv.second.pre_state);
     if (kv.second.copied) (void)hipEventDestroy(kv.second.copied);
   }
   h->sched.clear();
@@ -1458,6 +1474,42 @@ int do_render(vr_context *h, const vr_render_args *a, const vr_partition *part, 
       const uint32_t nb = bf[ki](P) * (P.views > 1 ? 2u : 1u);
       const uint64_t rot = (uint64_t)std::max(0, std::atoi(ev)) * nbx;
       P.block_rot = nb ? (uint32_t)(rot % nb) : 0u;
+    }
+    // the pre-leap launch (vr_march.hip preleap_kernel, round 6): scheduled tame launches with an
+    // occupancy map; its buffers live with the launch shape's schedule (one per stream)
+    if (VR_PRELEAP_LAUNCH && F.sched && F.sched->blocks && P.occ && P.tame && !P.pair_shift && P.fast_shade &&
+        !test_flag("VR_NO_PRELEAP")) {
+      vr_context::Schedule &S = *F.sched;
+      const uint32_t waves = S.blocks * (uint32_t)VR_WG_WAVES_HOST;
+      if (S.pre_waves != waves) {
+        if (S.pre_flag) (void)hipFree(S.pre_flag);
+        if (S.pre_state) (void)hipFree(S.pre_state);
+        S.pre_flag = nullptr;
+        S.pre_state = nullptr;
+        S.pre_waves = S.pre_cap = 0;
+        const uint32_t cap = std::max<uint32_t>(64u, waves / 8u);  // slots: an eighth of the waves
+        hipError_t e = S.pre_count ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&S.pre_count), 4);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.pre_flag), (size_t)waves * 4);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&S.pre_state), (size_t)cap * 64 * 2 * sizeof(float4));
+        if (e == hipSuccess) {
+          S.pre_waves = waves;
+          S.pre_cap = cap;
+        } else {
+          vr_host::consume(e, "hipMalloc (pre-leap buffers; the launch marches without)");
+        }
+      }
+      if (S.pre_waves == waves) {
+        P.pre_flag = S.pre_flag;
+        P.pre_state = S.pre_state;
+        P.pre_count = S.pre_count;
+        P.pre_cap = S.pre_cap;
+        typedef hipError_t (*pre_fn)(const vr::RenderParams &, hipStream_t);
+        static const pre_fn pfns[4] = {vr::fast::launch_preleap_k1, vr::fast::launch_preleap_k2,
+                                       vr::fast::launch_preleap_k4,
+                                       VR_K8(vr::fast::launch_preleap_k8, vr::fast::launch_preleap_k4)};
+        VR_HIP(hipMemsetAsync(S.pre_count, 0, 4, stream));
+        VR_HIP(pfns[ki](P, stream));
+      }
     }
     time_mark(h, 0, stream);
     {

@@ -2,6 +2,7 @@
 // (vr_kernels.hip).  Pure data; no torch types, no CUDA shims.
 #pragma once
 #include <stdint.h>
+#include <hip/hip_runtime.h>  // (float4)
 
 namespace vr {
 
@@ -128,6 +129,13 @@ struct RenderParams {
   float slab_z0, slab_z1, slab_margin;
   int32_t slab_pk0, slab_pk1, slab_dir;
   const float *slab_in;
+  // pre-leap (round 6, vr_march.hip preleap_kernel): per march wave (workgroup x 4 + wave) 0, or
+  // 1 + the slot whose 64 lanes' ray states (two float4 each: t, pos; sample index, alive | mine << 1)
+  // the march starts from; the slot counter and the number of slots
+  const uint32_t *pre_flag;
+  float4 *pre_state;
+  uint32_t *pre_count;
+  uint32_t pre_cap;
 };
 
 // The views of one multi-view launch (vr_render_channels), passed by value: 4 x 832 B of kernel

@@ -484,7 +484,7 @@ __device__ __forceinline__ void composite_group(const RenderParams &P, Ray &R, f
 template <int K, int MODE, bool AB_ALIAS, bool COUNT, bool SHARE2, bool BIG, bool NANCHK, int CAP, bool SLAB = false,
           int NL = 0>
 __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane, Ray &R, ChunkStats &C,
-                                      uint32_t kk = 0, KParams kp = nullptr) {
+                                      uint32_t kk = 0, KParams kp = nullptr, uint32_t gw = 0) {
   static_assert(!COUNT || K == 1 || VR_COUNT_K, "the counter variant is built for K = 1 only (VR_COUNT_K: all K)");
   static_assert(!SLAB || (!COUNT && BIG), "slab mode: no counters, 64-bit addressing");
   const int cap = P.max_steps;
@@ -547,52 +547,22 @@ __device__ __forceinline__ void march(const RenderParams &P, float *L, int lane,
       R.alive = R.alive && group_any<K>(R.mine);
     }
   };
-  // Per-lane pre-leap (round 6, VR_PRELEAP): a wave whose rays start far apart along their direction
-  // (t spread beyond VR_PRELEAP_SPREAD steps: a tile of rays entering the volume through a face at a
-  // grazing angle) cannot probe one box for them all, so before the march each ray walks the
-  // occupancy map along its own runs of VR_PROBE_MAX samples (probe_lane_walk) and leaps every run
-  // whose centre cells all lie in +-0 bricks -- exact as the probe's leap, run by run (the margin
-  // covers one run's drift) -- until a run finds data; a ray's K lanes leap together.  Rays that
-  // only graze empty space (rotate(30,10,0): the columns next to the silhouette, ~7000 empty samples
-  // each) end here; the rest start at their data, where wave-front parking aligns them.
+  // the state a pre-leap launch left for this wave (preleap_kernel), if any: the rays start there
   if constexpr (PROBE && VR_PRELEAP && !COUNT) {
-    if (kp != nullptr && kparams_fresh(kp)->occ != nullptr) {
-      const bool lv0 = K > 1 ? (R.alive && R.mine) : R.alive;
-      const int tmn = wave_min(lv0 ? __float_as_int(R.t) : 0x7f7fffff);
-      const int tmx = wave_max(lv0 ? __float_as_int(R.t) : 0);
-      if (__int_as_float(tmx) > __int_as_float(tmn) + (float)VR_PRELEAP_SPREAD * P.tstep) {
-        bool go = lv0;
-        while (group_any<K>(go)) {  // (a ray's K lanes decide together)
-          const KParams kq = kparams_fresh(kp);
-          uint32_t v = 0;
-          if (go) {
-            const float rem = (R.tfar - R.t) / kq->tstep;
-            const int s_eff = (rem < (float)VR_PROBE_MAX) ? max((int)rem + 2, 1) : (int)VR_PROBE_MAX;
-            const float k = (float)(s_eff - 1);
-            const f3 pe = mk(fmaf(R.step.x, k, R.pos.x), fmaf(R.step.y, k, R.pos.y), fmaf(R.step.z, k, R.pos.z));
-            v = probe_lane_walk(kq->occ, kq->occ_bx, kq->occ_bxy,
-                                ((R.pos.x - kq->bmin[0]) * kq->bscale[0]) * kq->em.fnx - 0.5f,
-                                ((R.pos.y - kq->bmin[1]) * kq->bscale[1]) * kq->em.fny - 0.5f,
-                                ((R.pos.z - kq->bmin[2]) * kq->bscale[2]) * kq->em.fnz - 0.5f,
-                                ((pe.x - kq->bmin[0]) * kq->bscale[0]) * kq->em.fnx - 0.5f,
-                                ((pe.y - kq->bmin[1]) * kq->bscale[1]) * kq->em.fny - 0.5f,
-                                ((pe.z - kq->bmin[2]) * kq->bscale[2]) * kq->em.fnz - 0.5f, kq->probe_off[0],
-                                kq->probe_off[1], kq->probe_off[2], kq->em.nx, kq->em.ny, kq->em.nz);
-          }
-          const bool data = group_any<K>(v != 0u);
-          if (go && !data) {
-            if constexpr (K == 1) {
-              advance_n(P, (int)VR_PROBE_MAX, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
-              go = R.alive;
-            } else {
-              advance_n(P, (int)VR_PROBE_MAX, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
-              go = group_any<K>(R.mine);
-            }
-          } else {
-            go = false;
-          }
+    if (kp != nullptr) {
+      const KParams kq = kparams_fresh(kp);
+      if (kq->pre_flag != nullptr) {
+        const uint32_t f = __builtin_amdgcn_readfirstlane(kq->pre_flag[gw]);
+        if (__builtin_expect(f != 0u, 0)) {
+          const float4 *st = kq->pre_state + ((size_t)(f - 1u) * 64u + (uint32_t)lane) * 2u;
+          const float4 a = st[0], b = st[1];
+          R.t = a.x;
+          R.pos = mk(a.y, a.z, a.w);
+          R.nsteps = __float_as_int(b.x);
+          const int fl = __float_as_int(b.y);
+          R.alive = (fl & 1) != 0;
+          R.mine = (fl & 2) != 0;
         }
-        if constexpr (K > 1) R.alive = R.alive && group_any<K>(R.mine);
       }
     }
   }
@@ -952,8 +922,8 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
   // every coordinate the march forms from a finite start and step is finite; a tame launch takes
   // the fast path (sample_at: TAME)
   if (P.tame && __all(!R.alive || (finite3(R.pos) && finite3(R.step))))
-    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP, false, NL>(P, L, lane, R, C, 0u,
-                                                                          (KParams)__builtin_amdgcn_kernarg_segment_ptr());
+    march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, false, CAP, false, NL>(
+        P, L, lane, R, C, 0u, (KParams)__builtin_amdgcn_kernarg_segment_ptr(), wgo * VR_WG_WAVES + (uint32_t)wave);
   else
     march<K, MODE, AB_ALIAS, COUNT, SHARE2, BIG, true, CAP>(P, L, lane, R, C);
 
@@ -993,6 +963,124 @@ __global__ __launch_bounds__(64 * VR_WG_WAVES, march_min_eu(CAP, SCHED)) void ma
     }
   }
 }
+
+// Pre-leap launch (round 6, VR_PRELEAP; DESIGN.md s5 "Rays far apart in one wave"): a wave whose
+// live rays start more than VR_PRELEAP_SPREAD steps apart along their direction (a tile of rays
+// entering the volume through a face at a grazing angle: the columns next to the silhouette at
+// rotate(30,10,0) start 900-2700 samples apart) cannot probe one box for them all, so before the
+// march each of its rays walks the occupancy map along its own runs of VR_PROBE_MAX samples
+// (probe_lane_walk: segments of at most 4 texels per axis, each segment's brick box widened by the
+// probe margin) and leaps every run whose cells all lie in +-0 bricks -- exact as the probe's leap,
+// run by run (the margin covers one run's drift) -- until a run finds data; a ray's K lanes leap
+// together.  The states go to a slot the march wave starts from (RenderParams::pre_flag / pre_state).
+// A separate launch: the same code inside the march cost every launch ~2 % (code placement), though
+// it rarely ran.  Same workgroups and ray mapping as march_kernel (not paired stereo tiles).
+template <int K>
+__global__ __launch_bounds__(64 * VR_WG_WAVES) void preleap_kernel(const RenderParams P) {
+  using TS = TileShape<K>;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t wgo = blockIdx.x;
+  const uint32_t gw = wgo * VR_WG_WAVES + (uint32_t)wave;
+  const int view = (P.views > 1 && wgo >= P.view_blocks) ? 1 : 0;
+  const uint32_t wg = view ? wgo - P.view_blocks : wgo;
+  const int tile = (int)wg * VR_WG_WAVES + wave;
+  const int nbx = (P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW);
+  const int blk = tile >> 2, quad = tile & 3;
+  const int ray = lane >> TS::LK;
+  const int lc = (blk % nbx) * (2 * TS::TW) + (quad & 1) * TS::TW + (ray / TS::TH);
+  const int y = (blk / nbx) * (2 * TS::TH) + (quad >> 1) * TS::TH + (ray % TS::TH);
+  const bool active = lc < P.part_cols && y < P.height;
+  Ray R;
+  R.pos = mk(0.f, 0.f, 0.f);
+  R.step = R.pos;
+  R.t = 0.f;
+  R.tfar = -1.f;
+  R.nsteps = 0;
+  R.alive = false;
+  if (active) {
+    const int pb = lc / P.block_cols, within = lc - pb * P.block_cols;
+    const int x = (P.part + pb * P.num_parts) * P.block_cols + within;
+    f3 o, d;
+    float tnear;
+    R.alive = ray_setup(P, x, y, o, d, tnear, R.tfar, view);
+    R.pos = mk(fmaf(d.x, tnear, o.x), fmaf(d.y, tnear, o.y), fmaf(d.z, tnear, o.z));
+    R.step = mk(d.x * P.tstep, d.y * P.tstep, d.z * P.tstep);
+    R.t = tnear;
+  }
+  const int cap = P.max_steps;
+  uint32_t flag = 0;
+  // the march's tame waves only (march_kernel: finite starts and steps; the probe needs the map)
+  if (P.tame && P.occ != nullptr && __all(!R.alive || (finite3(R.pos) && finite3(R.step)))) {
+    if constexpr (K > 1) {  // to this lane's first sample, as march()
+      R.mine = R.alive;
+      leap(P, lane & (K - 1), R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+      R.alive = group_any<K>(R.mine);
+    } else {
+      R.mine = R.alive;
+    }
+    const bool lv0 = K > 1 ? (R.alive && R.mine) : R.alive;
+    const int tmn = wave_min(lv0 ? __float_as_int(R.t) : 0x7f7fffff);
+    const int tmx = wave_max(lv0 ? __float_as_int(R.t) : 0);
+    if (__int_as_float(tmx) > __int_as_float(tmn) + (float)VR_PRELEAP_SPREAD * P.tstep) {
+      const KParams kq = (KParams)__builtin_amdgcn_kernarg_segment_ptr();
+      bool go = lv0;
+      while (group_any<K>(go)) {  // (a ray's K lanes decide together)
+        uint32_t v = 0;
+        if (go) {
+          const float rem = (R.tfar - R.t) / P.tstep;
+          const int s_eff = (rem < (float)VR_PROBE_MAX) ? max((int)rem + 2, 1) : (int)VR_PROBE_MAX;
+          const float k = (float)(s_eff - 1);
+          const f3 pe = mk(fmaf(R.step.x, k, R.pos.x), fmaf(R.step.y, k, R.pos.y), fmaf(R.step.z, k, R.pos.z));
+          v = probe_lane_walk(P.occ, P.occ_bx, P.occ_bxy, ((R.pos.x - P.bmin[0]) * P.bscale[0]) * P.em.fnx - 0.5f,
+                              ((R.pos.y - P.bmin[1]) * P.bscale[1]) * P.em.fny - 0.5f,
+                              ((R.pos.z - P.bmin[2]) * P.bscale[2]) * P.em.fnz - 0.5f,
+                              ((pe.x - P.bmin[0]) * P.bscale[0]) * P.em.fnx - 0.5f,
+                              ((pe.y - P.bmin[1]) * P.bscale[1]) * P.em.fny - 0.5f,
+                              ((pe.z - P.bmin[2]) * P.bscale[2]) * P.em.fnz - 0.5f, kq->probe_off[0],
+                              kq->probe_off[1], kq->probe_off[2], P.em.nx, P.em.ny, P.em.nz);
+        }
+        const bool data = group_any<K>(v != 0u);
+        if (go && !data) {
+          if constexpr (K == 1) {
+            advance_n(P, (int)VR_PROBE_MAX, R.alive, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+            go = R.alive;
+          } else {
+            advance_n(P, (int)VR_PROBE_MAX, R.mine, R.nsteps, R.t, R.tfar, R.pos, R.step, cap);
+            go = group_any<K>(R.mine);
+          }
+        } else {
+          go = false;
+        }
+      }
+      if constexpr (K > 1) R.alive = R.alive && group_any<K>(R.mine);
+      if constexpr (K == 1) R.mine = R.alive;
+      uint32_t slot = 0;
+      if (lane == 0) slot = atomicAdd(P.pre_count, 1u);
+      slot = __builtin_amdgcn_readfirstlane(slot);
+      if (slot < P.pre_cap) {  // (no slot left: the wave marches from its start, as without)
+        float4 *st = P.pre_state + ((size_t)slot * 64u + (uint32_t)lane) * 2u;
+        st[0] = make_float4(R.t, R.pos.x, R.pos.y, R.pos.z);
+        st[1] = make_float4(__int_as_float(R.nsteps), __int_as_float((R.alive ? 1 : 0) | (R.mine ? 2 : 0)), 0.f, 0.f);
+        flag = slot + 1u;
+      }
+    }
+  }
+  if (lane == 0) const_cast<uint32_t *>(P.pre_flag)[gw] = flag;
+}
+
+#if !VR_ISA_PROBE
+hipError_t VR_CAT(launch_preleap_k, VR_MARCH_K)(const RenderParams &P, hipStream_t s) {
+  constexpr int K = VR_MARCH_K;
+  using TS = TileShape<K>;
+  if (P.part_cols <= 0 || P.height <= 0) return hipSuccess;
+  if (!P.pre_flag || !P.pre_state || !P.pre_count || P.pair_shift) return hipErrorInvalidValue;
+  const uint64_t tiles = (uint64_t)((P.part_cols + 2 * TS::TW - 1) / (2 * TS::TW)) *
+                         (uint64_t)((P.height + 2 * TS::TH - 1) / (2 * TS::TH)) * 4;
+  const uint32_t per_view = (uint32_t)((tiles + VR_WG_WAVES - 1) / VR_WG_WAVES);
+  hipLaunchKernelGGL(preleap_kernel<K>, dim3(per_view * (P.views > 1 ? 2u : 1u)), dim3(64 * VR_WG_WAVES), 0, s, P);
+  return hipGetLastError();
+}
+#endif
 
 #if VR_MARCH_K <= 4
 // One wave's tile of workgroup `wg` of a view: ray setup, the march, the pixel store into `out` --
