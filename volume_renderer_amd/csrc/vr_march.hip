@@ -1332,7 +1332,9 @@ static bool inject_bad_launch() {
 // lights are hoisted (march: VR_LIGHTS_HOIST's conditions).
 template <int KK, int MODE, bool AB, bool CNT, bool SH, bool BG, int CAP, int SC>
 static void launch_one(const RenderParams &P, dim3 grid, dim3 blk, hipStream_t s) {
-  constexpr bool NL2 = VR_NL2 && VR_LIGHTS_HOIST && MODE != 0 && KK > 1 && AB && SH && !BG && !CNT;
+  // (on-the-fly gradient launches only: the lookup-gradient march, C3, measured 0.8 % slower with it,
+  // 27.65-27.70 vs 27.44-27.47 ms, r6v)
+  constexpr bool NL2 = VR_NL2 && VR_LIGHTS_HOIST && MODE == 1 && KK > 1 && AB && SH && !BG && !CNT;
   const int nl = (NL2 && (P.num_lights == 2 || P.num_lights == 1)) ? P.num_lights : 0;
   if (NL2 && nl == 2) hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC, NL2 ? 2 : 0>), grid, blk, 0, s, P);
   else if (NL2 && nl == 1) hipLaunchKernelGGL((march_kernel<KK, MODE, AB, CNT, SH, BG, CAP, SC, NL2 ? 1 : 0>), grid, blk, 0, s, P);
@@ -1460,7 +1462,7 @@ hipError_t VR_CAT(launch_march_k, VR_MARCH_K)(const RenderParams &P, int mode, b
 // ISA probe (tools/isa_probe.sh): only the metric frame's production instantiation and the matching
 // sort-last slab kernel, for a quick look at their code without compiling every variant.
 template __global__ void march_kernel<2, 1, true, false, true, false, VR_LDS_CAP_MARCH, 0, 2>(const RenderParams P);
-template __global__ void march_kernel<2, 2, true, false, true, false, VR_LDS_CAP, 0, 2>(const RenderParams P);  // C3
+template __global__ void march_kernel<2, 2, true, false, true, false, VR_LDS_CAP, 0, 0>(const RenderParams P);  // C3
 template __global__ void march_slab_kernel<2, 1, true, VR_LDS_CAP, false>(const RenderParams P);
 #endif  // !VR_ISA_PROBE
 }  // namespace fast / exact
