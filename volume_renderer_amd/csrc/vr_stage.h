@@ -280,6 +280,47 @@ __device__ __forceinline__ bool stage_box_elems(float *L, const DevTex &t, const
 }
 
 
+#ifndef VR_STAGE_GLDS
+#define VR_STAGE_GLDS 0  // (A/B) stage dense boxes with LDS-DMA loads (global_load_lds_dword)
+#endif
+
+// Copy a densely pitched box B into the slot with LDS-DMA loads: a dense slot is the box's V voxels
+// in x-fastest order, so slot words q0 .. q0 + 63 of one wave pass are the lane-linear destination
+// of one global_load_lds_dword (LDS address = slot + 4 q0 + 4 lane); no VGPR holds a voxel and no
+// ds_write is issued.  The non-zero test reads the slot back (one word per lane per pass).
+template <bool BIG>
+__device__ __forceinline__ bool stage_box_glds(float *L, const DevTex &t, const Box &B, int lane) {
+  const uint32_t ex = (uint32_t)B.ex, ey = (uint32_t)B.ey;
+  const uint32_t V = ex * ey * (uint32_t)B.ez;
+  uint32_t x = (uint32_t)lane % ex, r = (uint32_t)lane / ex;
+  uint32_t y = r % ey;
+  const float *src = t.p + ((uint64_t)(B.rz + r / ey) * t.pxy + (uint64_t)(B.ry + y) * t.px + (uint64_t)(B.rx + x));
+  const uint32_t sx = 64u % ex, sr = 64u / ex;
+  const int64_t g_step = (int64_t)sx + (int64_t)sr * (int64_t)t.px;
+  const int64_t g_row = (int64_t)t.px - (int64_t)ex, g_wrap = (int64_t)t.pxy - (int64_t)ey * (int64_t)t.px;
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the previous chunk's slot reads are done
+  for (uint32_t q0 = 0; q0 < V; q0 += 64u) {
+    if (q0 + (uint32_t)lane < V)
+      __builtin_amdgcn_global_load_lds((const void *)src, (__attribute__((address_space(3))) void *)(L + q0), 4, 0, 0);
+    x += sx;
+    y += sr;
+    src += g_step;
+    if (x >= ex) {
+      x -= ex;
+      ++y;
+      src += g_row;
+    }
+    while (y >= ey) {
+      y -= ey;
+      src += g_wrap;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the slot is written
+  uint32_t acc = 0;
+  for (uint32_t q = (uint32_t)lane; q < V; q += 64u) acc |= __float_as_uint(L[q]);
+  return __any((acc & 0x7fffffffu) != 0u);
+}
+
 // Copy box B of the apron volume into the wave's LDS slot (row-major, x fastest).  A wave pass
 // moves 64 / ex whole rows (lane -> (row slot, x)); row offsets advance incrementally, relative to
 // a wave-uniform base pointer, so a pass costs a handful of adds instead of per-element 64-bit
@@ -288,6 +329,9 @@ __device__ __forceinline__ bool stage_box_elems(float *L, const DevTex &t, const
 template <bool BIG>
 __device__ __forceinline__ bool stage_box(float *L, const DevTex &t, const Box &B, int lane) {
   const int ex = B.ex, ey = B.ey;
+  if (VR_STAGE_GLDS && B.px == ex && B.pxy == ex * ey &&
+      (BIG || (uint64_t)t.pxy * (uint64_t)B.ez * 4u < 0xFFFFFFFFull))
+    return stage_box_glds<BIG>(L, t, B, lane);
   if (ex > 64) return stage_box_elems(L, t, B, lane);
   if (!BIG && (uint64_t)t.pxy * (uint64_t)B.ez * 4u >= 0xFFFFFFFFull)  // 32-bit byte offsets overflow
     return stage_box_elems(L, t, B, lane);
